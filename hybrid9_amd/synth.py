@@ -1,0 +1,188 @@
+"""Synthetic HYBRID9 inputs (soil parameters, land mask, PGF-shaped forcing).
+
+The reference reads real datasets (BNU soil properties ``INIT.f90:492-633``,
+Fmax ``INIT.f90:652-680``, PGF v2.1 forcing ``READ_PGF.f90:22-109``) that are
+not available here, so every run uses this generator instead.
+
+Every value is a pure function of ``(seed, stream, key)`` through a
+splitmix64 mix, and every transform is a fixed sequence of float32
+operations with no transcendental calls, so this numpy version and the
+C/HIP version in ``hybrid9_amd/csrc/h9g_synth.h`` produce bit-identical
+arrays for any subset of cells or days (shards, sampled cells, fixtures).
+
+Layouts follow the reference (Fortran column-major, SURVEY.md §8 notation):
+per-layer parameters ``(L, ncell)`` layer-fastest -> numpy ``(ncell, L)``;
+forcing ``(ncell, ndays)`` per variable, cell-fastest -> numpy
+``(7, ndays, ncell)`` in the order of ``READ_PGF.f90``:
+tas, rlds, rsds, huss, ps, pr, rhs.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED = 20161123
+NX05, NY05, NLAND05 = 720, 360, 67_420          # 0.5 deg (CONTROL.f90:27-28)
+NX025, NY025, NLAND025 = 1440, 720, 270_000     # 0.25 deg (config 5)
+FORCING_VARS = ("tas", "rlds", "rsds", "huss", "ps", "pr", "rhs")
+
+# driver.txt:17-26 (zi(0:9), mm); config 5 uses 10 layers + aquifer.
+ZI_L8 = np.array([0.0, 45.0, 91.0, 166.0, 289.0, 493.0, 829.0, 1383.0,
+                  2296.0, 5000.0], dtype=np.float32)
+ZI_L10 = np.array([0.0, 18.0, 45.0, 91.0, 166.0, 289.0, 493.0, 829.0,
+                   1383.0, 2296.0, 3500.0, 5000.0], dtype=np.float32)
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+_STRM = np.uint64(0xD1B54A32D192ED03)
+
+# stream ids (must match h9g_synth.h)
+S_MASK, S_LAT = 1, 2
+S_THETA_S, S_KS, S_LAMBDA, S_PSI, S_FMAX, S_WET, S_PCELL = 10, 11, 12, 13, 14, 15, 16
+S_FORCING = 100          # + variable index, + 10 for the second draw of pr
+F32 = np.float32
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def u01(seed: int, stream: int, key) -> np.ndarray:
+    """Uniform float32 in [0, 1) with 24 random bits (exactly representable)."""
+    key = np.asarray(key, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) * _GOLD + np.uint64(stream) * _STRM + key)
+    return ((_mix64(z) >> np.uint64(40)).astype(np.float32)
+            * F32(1.0 / 16777216.0))
+
+
+# ----------------------------------------------------------------------------
+# land mask
+# ----------------------------------------------------------------------------
+def land_cells(nx: int = NX05, ny: int = NY05, nland: int = NLAND05,
+               seed: int = SEED) -> np.ndarray:
+    """Grid ids (iy*nx + ix, raster order as HYBRID9.f90:120-121) of the
+    ``nland`` synthetic land cells: the highest-scoring cells where the
+    score favours mid/high northern latitudes, roughly like Earth's land.
+    Deterministic; ties broken by grid id."""
+    gid = np.arange(nx * ny, dtype=np.uint64)
+    iy = (gid // np.uint64(nx)).astype(np.float64)
+    lat = 90.0 - (iy + 0.5) * (180.0 / ny)
+    w = np.where(lat < -60.0, 0.15, np.where(lat > 80.0, 0.2,
+                 0.45 + 0.35 * np.clip((lat + 10.0) / 70.0, 0.0, 1.0)))
+    score = u01(seed, S_MASK, gid).astype(np.float64) * w
+    order = np.lexsort((gid, -score))
+    return np.sort(order[:nland]).astype(np.int64)
+
+
+def cell_lat(gid, nx: int = NX05, ny: int = NY05) -> np.ndarray:
+    """Latitude of grid-box centres (INIT.f90:144-146 for 0.5 deg)."""
+    iy = (np.asarray(gid, dtype=np.int64) // nx).astype(np.float32)
+    dlat = F32(180.0 / ny)
+    return (F32(90.0) - dlat * F32(0.5)) - iy * dlat
+
+
+# ----------------------------------------------------------------------------
+# soil parameters (units after INIT.f90:611-631 conversion)
+# ----------------------------------------------------------------------------
+def make_params(gid, nlayers: int = 8, seed: int = SEED) -> dict:
+    gid = np.asarray(gid, dtype=np.uint64)
+    n = gid.size
+    lay = np.arange(nlayers, dtype=np.uint64)
+    key = gid[:, None] * np.uint64(16) + lay[None, :]
+    theta_s = F32(0.30) + F32(0.30) * u01(seed, S_THETA_S, key)
+    ks = F32(0.5) + F32(487.5) * u01(seed, S_KS, key)            # cm/day
+    hksat = (F32(10.0) * ks) / F32(86400.0)                        # mm/s
+    lam = F32(0.10) + F32(0.40) * u01(seed, S_LAMBDA, key)
+    lam = np.maximum(lam, F32(1.0e-8))                             # trunc
+    bsw = F32(1.0) / lam
+    psi = F32(-80.0) + F32(75.0) * u01(seed, S_PSI, key)          # cm
+    psi_s = F32(10.0) * psi                                        # mm
+    fmax = F32(0.1) + F32(0.5) * u01(seed, S_FMAX, gid)
+    out = dict(theta_s=theta_s, hksat=hksat, bsw=bsw, psi_s=psi_s,
+               fmax=fmax.astype(np.float32))
+    for k in ("theta_s", "hksat", "bsw", "psi_s"):
+        out[k] = np.ascontiguousarray(out[k].astype(np.float32).reshape(n, nlayers))
+    return out
+
+
+# ----------------------------------------------------------------------------
+# forcing
+# ----------------------------------------------------------------------------
+def make_forcing(gid, lat, day0: int, ndays: int, seed: int = SEED) -> np.ndarray:
+    """Forcing for days ``day0 .. day0+ndays-1`` (day 0 = 1 Jan 1901).
+
+    Returns float32 ``(7, ndays, ncell)`` in READ_PGF order."""
+    gid = np.asarray(gid, dtype=np.uint64)
+    lat = np.asarray(lat, dtype=np.float32)
+    n = gid.size
+    d = np.arange(day0, day0 + ndays, dtype=np.int64)
+    key = (d.astype(np.uint64)[:, None] << np.uint64(32)) | gid[None, :]
+
+    alat = np.abs(lat)[None, :]
+    hs = np.where(lat >= F32(0.0), F32(-1.0), F32(1.0)).astype(np.float32)[None, :]
+    f = (d % 365).astype(np.float32)[:, None] / F32(365.0)
+    tri = F32(4.0) * np.abs(f - F32(0.5)) - F32(1.0)
+    season = hs * tri                                  # +1 local mid-summer
+    wet = u01(seed, S_WET, gid)[None, :]
+    pcell = (F32(65000.0) + F32(38000.0) * u01(seed, S_PCELL, gid))[None, :]
+
+    def uu(v):
+        return u01(seed, S_FORCING + v, key)
+
+    tmean = F32(303.0) - F32(0.55) * alat
+    amp = F32(0.25) * alat
+    tas = tmean + amp * season + F32(6.0) * (uu(0) - F32(0.5))
+    tas = np.minimum(np.maximum(tas, F32(240.0)), F32(315.0))
+    rlds = F32(250.0) + F32(2.5) * (tas - F32(273.0)) + F32(60.0) * (uu(1) - F32(0.5))
+    rlds = np.minimum(np.maximum(rlds, F32(150.0)), F32(450.0))
+    rsds = (F32(180.0) + F32(100.0) * season * (alat / F32(80.0))
+            - alat + F32(120.0) * (uu(2) - F32(0.5)))
+    rsds = np.minimum(np.maximum(rsds, F32(0.0)), F32(350.0))
+    warm = np.maximum(F32(0.0), (tas - F32(240.0)) / F32(70.0))
+    huss = F32(1.0e-4) + F32(0.015) * uu(3) * warm
+    ps = pcell + F32(800.0) * (uu(4) - F32(0.5))
+    prain = F32(0.15) + F32(0.5) * wet
+    rate = F32(2.0e-4) * wet + F32(2.0e-5)
+    u2 = u01(seed, S_FORCING + 15, key)
+    pr = np.where(uu(5) < prain, F32(3.0) * rate * (u2 * u2), F32(0.0))
+    rhs = F32(10.0) + F32(90.0) * uu(6)
+    out = np.stack([tas, rlds, rsds, huss, ps, pr, rhs]).astype(np.float32)
+    assert out.shape == (7, ndays, n)
+    return out
+
+
+# ----------------------------------------------------------------------------
+# calendar (INIT.f90:844-859)
+# ----------------------------------------------------------------------------
+def time_boy() -> np.ndarray:
+    """time_BOY(jyear-1859), 1-based by year index: returns array t with
+    t[jyear - 1860] = first iTIME of jyear (iTIME 1 = 1 Jan 1860)."""
+    t = np.zeros(2300 - 1860 + 1, dtype=np.int64)
+    t[0] = 1
+    for jyear in range(1861, 2301):
+        y = jyear - 1
+        if y % 4 != 0:
+            inc = 365
+        elif y % 100 != 0:
+            inc = 366
+        elif y % 400 != 0:
+            inc = 365
+        else:
+            inc = 366
+        t[jyear - 1860] = t[jyear - 1861] + inc
+    return t
+
+
+_TBOY = time_boy()
+
+
+def year_day0(year: int) -> int:
+    """Global day index (0 = 1 Jan 1901) of 1 Jan ``year``."""
+    return int(_TBOY[year - 1860] - _TBOY[1901 - 1860])
+
+
+def days_in_year(year: int) -> int:
+    return int(_TBOY[year + 1 - 1860] - _TBOY[year - 1860])

@@ -1,0 +1,68 @@
+/*
+ * TEST INFRASTRUCTURE ONLY -- the CPU oracle (plain C restatement).
+ *
+ * A line-by-line restatement, in C, of HYBRID9's per-cell hot path:
+ *   HYDROLOGY  /root/reference/SOURCE/HYDROLOGY.f90:141-1283
+ *   GROW       /root/reference/SOURCE/GROW.f90:55-201
+ *   day driver /root/reference/SOURCE/HYBRID9.f90:120-290
+ *   state init /root/reference/SOURCE/INIT.f90:707-811
+ * calling glibc expf/powf exactly where the reference does (flang lowers
+ * EXP and real powers to expf/powf; MIN/MAX to compare+select, see oracle/README.md).
+ * Compiled with -ffp-contract=off (the reference executes no FMA).
+ *
+ * Pinned bit-for-bit against oracle/_ref/h9ref (the reference's own
+ * HYDROLOGY/GROW) through tests/golden (see tests/test_oracle_golden.py).
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * may load this library, as the checker -- never as the product.
+ *
+ * Semantics: isolated-cell (each cell carries its own hidden smp).
+ * Layouts: see oracle/refcase.py.  L <= H9O_LMAX soil layers.
+ */
+#ifndef H9_ORACLE_H
+#define H9_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define H9O_LMAX 16
+#define H9O_NANNUAL_SCALARS 11
+
+/* STOP sites of the reference (HYDROLOGY.f90:806-825,1068-1072,1244-1274) */
+enum { H9O_OK = 0, H9O_ERR_TRIDIAG1 = 1, H9O_ERR_TRIDIAG2 = 2,
+       H9O_ERR_RSUB_POS = 3, H9O_ERR_IMBALANCE = 4, H9O_ERR_ARGS = 10 };
+
+typedef struct {
+  int code;      /* first failure, H9O_ERR_* */
+  int cell;      /* 0-based cell index */
+  int day;       /* 0-based day within the run */
+  int substep;   /* 0-based substep */
+  float value;   /* w1-w0, BET, ... */
+} h9o_error;
+
+/* floats per cell of the packed state (refcase.state_fields) */
+int h9o_state_size(int L);
+
+/* INIT.f90:707-811 initial state for every cell (smp = 0). */
+int h9o_init_state(int ncell, int L, const float *zi, const float *params,
+                   float *state);
+
+/* Run nyears calendar years from year0 for every cell.
+ *   zi       L+2 floats, zi(0:L+1)
+ *   params   theta_s, hksat, bsw, psi_s (ncell*L each, layer-fastest), fmax
+ *   forcing  (7, ndays, ncell), ndays = days in [year0, year0+nyears)
+ *   state    in/out packed state (h9o_state_size(L) * ncell floats)
+ *   annual   out (nyears, 12+L, ncell)
+ *   trace    optional: for each of the ntrace cells, every substep,
+ *            3L+7 floats (refcase.trace_width)
+ *   nthreads OpenMP threads over cells (<=0: default)
+ * Returns 0, or the first H9O_ERR_* (details in *err if non-NULL). */
+int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
+            const float *zi, const float *params, const float *forcing,
+            float *state, float *annual, int ntrace, const int *trace_cells,
+            float *trace, int nthreads, h9o_error *err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,91 @@
+"""TEST INFRASTRUCTURE ONLY: ctypes binding of the C oracle (oracle/h9_oracle.c).
+
+Used by tests/ (as the checker), __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  The product never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+from . import refcase
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "_build" / "libh9oracle.so"
+_lib = None
+
+
+class H9OError(C.Structure):
+    _fields_ = [("code", C.c_int), ("cell", C.c_int), ("day", C.c_int),
+                ("substep", C.c_int), ("value", C.c_float)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(HERE), "port"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        _lib = C.CDLL(str(LIB))
+        f = C.POINTER(C.c_float)
+        _lib.h9o_state_size.argtypes = [C.c_int]
+        _lib.h9o_init_state.argtypes = [C.c_int, C.c_int, f, f, f]
+        _lib.h9o_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 f, f, f, f, f, C.c_int, C.POINTER(C.c_int), f,
+                                 C.c_int, C.POINTER(H9OError)]
+    return _lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def pack_params(params) -> np.ndarray:
+    return np.concatenate([params[k].ravel() for k in ("theta_s", "hksat", "bsw", "psi_s")]
+                          + [params["fmax"].ravel()]).astype(np.float32)
+
+
+def init_state(params, zi) -> np.ndarray:
+    L = params["theta_s"].shape[1]
+    n = params["fmax"].size
+    st = np.zeros(n * lib().h9o_state_size(L), dtype=np.float32)
+    pp = pack_params(params)
+    zi = np.ascontiguousarray(zi, dtype=np.float32)
+    rc = lib().h9o_init_state(n, L, _fp(zi), _fp(pp), _fp(st))
+    assert rc == 0
+    return st
+
+
+def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=1,
+        state0=None, trace_cells=(), nthreads=1):
+    """Same contract as refcase.run_case; returns dict(annual, state, trace?, err)."""
+    L = params["theta_s"].shape[1]
+    n = params["fmax"].size
+    zi = np.ascontiguousarray(zi, dtype=np.float32)
+    pp = pack_params(params)
+    fo = np.ascontiguousarray(forcing, dtype=np.float32)
+    if state0 is None:
+        st = init_state(params, zi)
+    else:
+        st = refcase.pack_state(state0, L)
+    ann = np.zeros((nyears, 12 + L, n), dtype=np.float32)
+    ndays = fo.shape[1]
+    tc = np.asarray(sorted(trace_cells), dtype=np.int32)
+    tr = np.zeros((max(len(tc), 1), ndays * nisurf, refcase.trace_width(L)), dtype=np.float32)
+    err = H9OError()
+    rc = lib().h9o_run(n, L, nisurf, int(grow_on), year0, nyears, _fp(zi), _fp(pp), _fp(fo),
+                       _fp(st), _fp(ann), len(tc), tc.ctypes.data_as(C.POINTER(C.c_int)),
+                       _fp(tr), nthreads, C.byref(err))
+    out = dict(annual=ann, state=refcase.unpack_state(st, n, L), rc=rc,
+               err=dict(code=err.code, cell=err.cell, day=err.day, substep=err.substep,
+                        value=err.value))
+    if len(tc):
+        out["trace"] = tr
+    return out
