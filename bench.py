@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""HYBRID9 hot-path benchmark on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2]
+
+A *step* is one simulated calendar year for every land cell of the GPU:
+365/366 days x NISURF substeps of HYDROLOGY (+ daily GROW when enabled),
+i.e. one ``h9g_run_year`` launch, followed by the per-year FP64 diagnostics
+that are all-reduced across GPUs over RCCL (torch.distributed "nccl").
+Inputs (soil parameters, a distinct forcing year per step) are generated on
+the device and resident in HBM before the timed region.  Weak scaling: each
+rank simulates the full synthetic 0.5 deg land grid with its own seed
+(SURVEY.md §8e).  Rank 0 prints one JSON line.
+
+``value`` = cell-steps/s over all ranks (cells x days x NISURF x K / max
+rank time).  ``roofline.achieved`` = the SURVEY.md §8d algorithmic bytes of
+the per-substep SHARED-state contract (4(10L+14) B/cell-step) per launch /
+the launch's device time from HIP events on the kernel's stream.
+``cpu_baseline`` times the reference itself (oracle/_ref/h9ref: unmodified
+HYDROLOGY.f90 compiled with amdflang) on a bounded sample of the same
+workload, one process per host core, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "grid-cell-steps/sec at 0.5° global (1/2/4/8 GPUs) + achieved HBM GB/s"
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOADS = {
+    # BASELINE.json configs[1]: the metric's config (fits one GPU)
+    "config2": dict(desc="0.5deg global synthetic land, 67,420 cells/GPU, daily forcing, "
+                         "NISURF=48, hydrology-only (GROW off), L=8",
+                    grid="05", nlayers=8, nisurf=48, grow_on=False),
+    "config3": dict(desc="0.5deg global synthetic land, 67,420 cells/GPU, NISURF=24, "
+                         "HYDROLOGY+GROW coupled, L=8",
+                    grid="05", nlayers=8, nisurf=24, grow_on=True),
+    "config5": dict(desc="0.25deg global synthetic land, 270,000 cells, 10 layers, NISURF=24, "
+                         "GROW on",
+                    grid="025", nlayers=10, nisurf=24, grow_on=True),
+}
+
+
+def bytes_per_cell_step(L: int) -> int:
+    """reads 8 per-layer arrays + 5 scalars + 7 forcing,
+    writes 2 per-layer arrays + 2 scalars -> 4 (10 L + 14) bytes."""
+    return 4 * (10 * L + 14)
+
+
+def dist_setup(n_gpus: int):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}; launch N>1 with torchrun")
+    torch = dist = None
+    try:
+        import torch  # noqa: F811
+        import torch.distributed as dist  # noqa: F811
+    except Exception:                        # torch is plumbing only
+        if world > 1:
+            raise
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")      # RCCL over xGMI on ROCm
+    return rank, world, local, torch, dist
+
+
+def barrier_sync(ctx, torch, dist, world):
+    ctx.sync()
+    if torch is not None and torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+
+
+def cpu_baseline(workload: dict, seed: int) -> dict:
+    """The reference (oracle/_ref/h9ref) on a bounded sample of the same
+    workload: P processes x C cells x 1 year, like `mpirun -np P` without MPI
+    (the reference's ranks never communicate during compute)."""
+    from hybrid9_amd import synth
+    from oracle import refcase
+
+    P = int(os.environ.get("H9_CPU_PROCS", os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    P = max(1, min(P, os.cpu_count() or 1, 64))
+    C = int(os.environ.get("H9_CPU_CELLS", "512"))
+    L, ns, grow = workload["nlayers"], workload["nisurf"], int(workload["grow_on"])
+    kind = "reference" if refcase.REF_BIN.exists() and L == 8 else "port"
+    land = synth.land_cells()
+    nt = synth.days_in_year(1901)
+    tmp = Path(tempfile.mkdtemp(prefix="h9cpu_"))
+    dirs = []
+    for i in range(P):
+        g = land[(i * 7919) % (land.size - C):][:C]
+        p = synth.make_params(g, L, seed)
+        f = synth.make_forcing(g, synth.cell_lat(g), 0, nt, seed)
+        d = tmp / f"p{i}"
+        refcase.write_case(d, zi=synth.ZI_L8, params=p, forcing=f, nisurf=ns, grow_on=grow)
+        dirs.append((d, p, f))
+    t0 = time.perf_counter()
+    if kind == "reference":
+        procs = [subprocess.Popen([str(refcase.REF_BIN), str(d)], stdout=subprocess.PIPE,
+                                  stderr=subprocess.STDOUT) for d, _, _ in dirs]
+        outs = [pr.communicate()[0].decode() for pr in procs]
+        wall = time.perf_counter() - t0
+        ok = all(pr.returncode == 0 and "STOP" not in o for pr, o in zip(procs, outs))
+    else:
+        from oracle import port
+        for d, p, f in dirs:
+            port.run(zi=synth.ZI_L8, params=p, forcing=f, nisurf=ns, grow_on=grow, nthreads=1)
+        wall = time.perf_counter() - t0
+        P = 1
+        ok = True
+    steps = P * C * nt * ns
+    subprocess.run(["rm", "-rf", str(tmp)])
+    return {"value": steps / wall, "unit": "cell-steps/s", "cores": P, "kind": kind,
+            "sample": f"{'reference HYDROLOGY.f90 (amdflang -O2)' if kind == 'reference' else 'C port'}"
+                      f" x {P} processes x {C} cells x 1 yr ({ns} substeps/day, GROW "
+                      f"{'on' if grow else 'off'}) = {steps:.3e} cell-steps in {wall:.1f} s"
+                      f"{'' if ok else ' (a sample process STOPped)'}"}
+
+
+def load_traffic(workload_name: str):
+    """HBM traffic per launch measured with rocprofv3 PMC counters
+    (profiles/pmc_*.json, written by tools/pmc_traffic.py)."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob("pmc_*.json")):
+        try:
+            d = json.loads(p.read_text())
+        except Exception:
+            continue
+        if d.get("workload") == workload_name:
+            best = d
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=None)
+    args = ap.parse_args()
+
+    rank, world, local, torch, dist = dist_setup(args.gpus)
+    import hybrid9_amd as h
+    from hybrid9_amd import synth
+
+    wl = WORKLOADS[args.workload]
+    L, ns = wl["nlayers"], wl["nisurf"]
+    if wl["grid"] == "05":
+        gid = synth.land_cells()
+        lat = synth.cell_lat(gid)
+        zi = synth.ZI_L8
+    else:
+        gid = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)
+        lat = synth.cell_lat(gid, synth.NX025, synth.NY025)
+        zi = synth.ZI_L10
+    seed = (args.seed if args.seed is not None else synth.SEED) + rank   # weak scaling
+    K, W = args.steps, args.warmup
+    years = [1901 + i for i in range(W + K)]
+
+    ctx = h.Context(gid.size, zi, nlayers=L, nisurf=ns, grow_on=wl["grow_on"],
+                    nslots=W + K, device=local if world > 1 else 0)
+    ctx.set_cells(gid, lat)
+    ctx.synth_params(seed)
+    ctx.init_state()
+    for s, y in enumerate(years):                  # forcing resident in HBM
+        ctx.synth_forcing(s, seed, synth.year_day0(y), synth.days_in_year(y))
+    ctx.sync()
+
+    diag_t = None
+    if world > 1:
+        diag_t = torch.zeros(h.NDIAG, dtype=torch.float64, device=f"cuda:{local}")
+
+    def step(s, y):
+        ctx.run_year(s, y)
+        if world > 1:
+            ctx.get_diagnostics(dev_ptr=diag_t.data_ptr())
+            dist.all_reduce(diag_t)                # RCCL: global diagnostics only
+            return None
+        return ctx.get_diagnostics()
+
+    for s in range(W):
+        step(s, years[s])
+    barrier_sync(ctx, torch, dist, world)
+    ctx.total_kernel_ms(reset=True)
+    t0 = time.perf_counter()
+    diag = None
+    for k in range(K):
+        diag = step(W + k, years[W + k])
+    barrier_sync(ctx, torch, dist, world)
+    elapsed = time.perf_counter() - t0
+    kern_ms = ctx.total_kernel_ms(reset=True)
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+        diag = diag_t.cpu().numpy()
+
+    cell_steps_rank = sum(gid.size * synth.days_in_year(y) * ns for y in years[W:])
+    value = world * cell_steps_rank / elapsed
+    launch_s = kern_ms / 1e3 / K
+    algo_bytes_launch = cell_steps_rank / K * bytes_per_cell_step(L)
+    achieved = algo_bytes_launch / launch_s / 1e9
+    pmc = load_traffic(args.workload)
+    traffic = None
+    if pmc and pmc.get("hbm_bytes_per_launch"):
+        traffic = pmc["hbm_bytes_per_launch"] / launch_s / 1e9
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "cell-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (hybrid9_amd.synth seed %d+rank, generated on device; PGF/BNU "
+                "datasets are not available offline)" % (synth.SEED if args.seed is None else args.seed),
+        "config": {"workload": f"{args.workload}: {wl['desc']}", "cells_per_gpu": int(gid.size),
+                   "nlayers": L, "nisurf": ns, "grow": wl["grow_on"],
+                   "years_per_step": 1, "parallelism": f"dp{world} (cell shards, RCCL all-reduce "
+                   "of FP64 diagnostics per year)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": ctx.kernel_name(), "kernel_ms_per_launch": launch_s * 1e3,
+                     "algorithmic_bytes_per_launch": algo_bytes_launch,
+                     "traffic_source": (pmc or {}).get("source")},
+        "cpu_baseline": None,
+        "diagnostics_last_year": {k: float(v) for k, v in zip(h.DIAG_NAMES, diag)},
+    }
+    ctx.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(wl, synth.SEED)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,313 @@
+"""hybrid9_amd -- MI355X-native HYBRID9 per-cell hydrology/vegetation hot path.
+
+Python host mirror of the C-ABI in ``include/h9g.h`` (``lib/libh9g.so``,
+built by ``hybrid9_amd.build``).  The reference has no Python surface: its
+only "interface" is the driver loop ``HYBRID9.f90:120-295`` around the
+argument-less ``SUBROUTINE HYDROLOGY``/``GROW``.  ``Context`` exposes that
+loop one calendar year at a time, with the reference's array layouts and
+STOP conditions (raised as :class:`ReferenceStop` carrying the first failing
+cell, like the reference's diagnostics block ``HYDROLOGY.f90:1244-1274``).
+
+There is no CPU fallback: if the HIP library is missing or cannot reach a
+GPU, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "lib" / "libh9g.so"
+NFORCING = 7
+NANNUAL_SCALARS = 11
+NDIAG = 12
+ANNUAL_SCALARS = ("npp", "plant_mass", "rnf", "evap", "tas", "rlds", "rsds",
+                  "huss", "ps", "pr", "rhs")
+DIAG_NAMES = ("cells", "rnf_sum", "theta_total_sum", "zwt_sum", "wa_sum",
+              "npp_sum", "plant_mass_sum", "lai_sum", "theta1_sum", "tas_sum",
+              "pr_sum", "failed_cells")
+STOP_MESSAGES = {  # HYDROLOGY.f90 STOP sites
+    1: "Problem with tridiagonal 1.",            # :806-812
+    2: "Problem with tridiagonal 2.",            # :818-825
+    3: "rsub_top_tot is positive in drainage",   # :1068-1072
+    4: "Problem in HYDROLOGY: Water imbalance > 0.1 mm",  # :1244-1274
+}
+LMAX = 10
+
+
+class H9GError(RuntimeError):
+    """API / HIP failure (negative return codes)."""
+
+
+class ReferenceStop(RuntimeError):
+    """A cell hit one of the reference's STOP conditions."""
+
+    def __init__(self, err: dict):
+        self.err = err
+        msg = STOP_MESSAGES.get(err["code"], f"code {err['code']}")
+        super().__init__(f"{msg} cell={err['cell']} year={err['year']} "
+                         f"day={err['day']} substep={err['substep']} value={err['value']}")
+
+
+class _Config(C.Structure):
+    _fields_ = [("ncell", C.c_int32), ("nlayers", C.c_int32), ("nisurf", C.c_int32),
+                ("grow_on", C.c_int32), ("max_days", C.c_int32), ("nslots", C.c_int32),
+                ("zi", C.c_float * (LMAX + 2))]
+
+
+class _Error(C.Structure):
+    _fields_ = [("code", C.c_int32), ("cell", C.c_int32), ("year", C.c_int32),
+                ("day", C.c_int32), ("substep", C.c_int32), ("value", C.c_float)]
+
+
+_lib = None
+_FP = C.POINTER(C.c_float)
+_DP = C.POINTER(C.c_double)
+_I64P = C.POINTER(C.c_int64)
+
+
+def lib() -> C.CDLL:
+    """Load libh9g.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise H9GError(f"{LIB_PATH} not built: run `python -m hybrid9_amd.build` "
+                       "(or __graft_entry__.build())")
+    L = C.CDLL(str(LIB_PATH))
+    vp = C.c_void_p
+    sig = {
+        "h9g_abi_version": (C.c_int, []),
+        "h9g_device_count": (C.c_int, []),
+        "h9g_create": (vp, [C.POINTER(_Config), C.c_int]),
+        "h9g_destroy": (None, [vp]),
+        "h9g_set_params": (C.c_int, [vp, _FP, _FP, _FP, _FP, _FP]),
+        "h9g_init_state": (C.c_int, [vp]),
+        "h9g_state_size": (C.c_int, [C.c_int]),
+        "h9g_set_state": (C.c_int, [vp, _FP]),
+        "h9g_get_state": (C.c_int, [vp, _FP]),
+        "h9g_push_forcing": (C.c_int, [vp, C.c_int, C.c_int, _FP, C.c_int]),
+        "h9g_push_forcing_device": (C.c_int, [vp, C.c_int, C.c_int, vp]),
+        "h9g_forcing_slot": (vp, [vp, C.c_int]),
+        "h9g_host_alloc": (vp, [C.c_size_t]),
+        "h9g_host_free": (None, [vp]),
+        "h9g_run_year": (C.c_int, [vp, C.c_int, C.c_int]),
+        "h9g_sync": (C.c_int, [vp]),
+        "h9g_last_error": (C.c_int, [vp, C.POINTER(_Error)]),
+        "h9g_get_annual": (C.c_int, [vp, _FP]),
+        "h9g_get_diagnostics": (C.c_int, [vp, _DP, vp]),
+        "h9g_set_cells": (C.c_int, [vp, _I64P, _FP]),
+        "h9g_synth_params": (C.c_int, [vp, C.c_uint64]),
+        "h9g_synth_forcing": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_int, C.c_int]),
+        "h9g_last_kernel_ms": (C.c_float, [vp]),
+        "h9g_total_kernel_ms": (C.c_double, [vp, C.c_int]),
+        "h9g_kernel_name": (C.c_char_p, [vp]),
+        "h9g_math_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP]),
+        "h9g_synth_host": (C.c_int, [C.c_uint64, C.c_int, C.c_int, _I64P, _FP, C.c_int,
+                                     C.c_int, _FP, _FP]),
+        "h9g_host_expf": (C.c_float, [C.c_float]),
+        "h9g_host_powf": (C.c_float, [C.c_float, C.c_float]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.h9g_abi_version() != 1:
+        raise H9GError("libh9g ABI mismatch")
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    """Names every C-ABI entry point declared in include/h9g.h."""
+    import re
+    hdr = (HERE.parent / "include" / "h9g.h").read_text()
+    return sorted(set(re.findall(r"\b(h9g_[a-z_0-9]+)\s*\(", hdr)))
+
+
+def _fp(a):
+    return a.ctypes.data_as(_FP)
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise H9GError(f"{what} failed with {rc}")
+    return rc
+
+
+def days_in_year(y: int) -> int:
+    """INIT.f90:844-859 calendar (Gregorian)."""
+    if y % 4:
+        return 365
+    if y % 100:
+        return 366
+    if y % 400:
+        return 365
+    return 366
+
+
+def state_size(L: int) -> int:
+    return 4 * L + 9
+
+
+class Context:
+    """One GPU, one shard of land cells (C-ABI ``h9g_ctx``)."""
+
+    def __init__(self, ncell: int, zi, *, nlayers: int = 8, nisurf: int = 48,
+                 grow_on: bool = True, max_days: int = 366, nslots: int = 2,
+                 device: int = 0):
+        lb = lib()
+        zi = np.asarray(zi, dtype=np.float32)
+        if zi.size != nlayers + 2:
+            raise ValueError(f"zi must hold zi(0:L+1) = {nlayers + 2} values")
+        cfg = _Config()
+        cfg.ncell, cfg.nlayers, cfg.nisurf = int(ncell), int(nlayers), int(nisurf)
+        cfg.grow_on, cfg.max_days, cfg.nslots = int(bool(grow_on)), int(max_days), int(nslots)
+        for i, v in enumerate(zi):
+            cfg.zi[i] = float(v)
+        self._lib = lb
+        self.ncell, self.L, self.nisurf, self.grow_on = int(ncell), int(nlayers), int(nisurf), bool(grow_on)
+        self.zi = zi
+        self.device = device
+        self._keep = {}
+        self._h = lb.h9g_create(C.byref(cfg), int(device))
+        if not self._h:
+            raise H9GError(f"h9g_create failed (ncell={ncell}, L={nlayers}, device={device}); "
+                           "is a gfx950 GPU visible?")
+
+    # -- lifetime ---------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.h9g_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- parameters & state -----------------------------------------------
+    def set_params(self, params: dict):
+        """params: theta_s, hksat, bsw, psi_s as (ncell, L); fmax (ncell)."""
+        arrs = [np.ascontiguousarray(params[k], dtype=np.float32)
+                for k in ("theta_s", "hksat", "bsw", "psi_s", "fmax")]
+        for a in arrs[:4]:
+            assert a.shape == (self.ncell, self.L), a.shape
+        assert arrs[4].shape == (self.ncell,)
+        _check(self._lib.h9g_set_params(self._h, *[_fp(a) for a in arrs]), "h9g_set_params")
+
+    def init_state(self):
+        _check(self._lib.h9g_init_state(self._h), "h9g_init_state")
+
+    def set_state(self, packed: np.ndarray):
+        packed = np.ascontiguousarray(packed, dtype=np.float32)
+        assert packed.size == state_size(self.L) * self.ncell
+        _check(self._lib.h9g_set_state(self._h, _fp(packed)), "h9g_set_state")
+
+    def get_state(self) -> np.ndarray:
+        out = np.empty(state_size(self.L) * self.ncell, dtype=np.float32)
+        _check(self._lib.h9g_get_state(self._h, _fp(out)), "h9g_get_state")
+        return out
+
+    # -- forcing ----------------------------------------------------------
+    def push_forcing(self, slot: int, forcing: np.ndarray, async_: bool = False):
+        """forcing: (7, nday, ncell) float32 in READ_PGF order."""
+        forcing = np.ascontiguousarray(forcing, dtype=np.float32)
+        assert forcing.shape[0] == NFORCING and forcing.shape[2] == self.ncell, forcing.shape
+        self._keep[slot] = forcing        # async copies read it after return
+        _check(self._lib.h9g_push_forcing(self._h, slot, forcing.shape[1], _fp(forcing),
+                                          int(async_)), "h9g_push_forcing")
+
+    def push_forcing_device(self, slot: int, nday: int, dev_ptr: int):
+        _check(self._lib.h9g_push_forcing_device(self._h, slot, nday, C.c_void_p(dev_ptr)),
+               "h9g_push_forcing_device")
+
+    def set_cells(self, gid, lat):
+        gid = np.ascontiguousarray(gid, dtype=np.int64)
+        lat = np.ascontiguousarray(lat, dtype=np.float32)
+        assert gid.size == lat.size == self.ncell
+        _check(self._lib.h9g_set_cells(self._h, gid.ctypes.data_as(_I64P), _fp(lat)),
+               "h9g_set_cells")
+
+    def synth_params(self, seed: int):
+        _check(self._lib.h9g_synth_params(self._h, C.c_uint64(seed)), "h9g_synth_params")
+
+    def synth_forcing(self, slot: int, seed: int, day0: int, nday: int):
+        _check(self._lib.h9g_synth_forcing(self._h, slot, C.c_uint64(seed), day0, nday),
+               "h9g_synth_forcing")
+
+    # -- hot path ---------------------------------------------------------
+    def run_year(self, slot: int, jyear: int):
+        _check(self._lib.h9g_run_year(self._h, slot, jyear), "h9g_run_year")
+
+    def sync(self, raise_on_stop: bool = True) -> int:
+        rc = _check(self._lib.h9g_sync(self._h), "h9g_sync")
+        if rc and raise_on_stop:
+            raise ReferenceStop(self.last_error())
+        return rc
+
+    def last_error(self) -> dict:
+        e = _Error()
+        _check(self._lib.h9g_last_error(self._h, C.byref(e)), "h9g_last_error")
+        return dict(code=e.code, cell=e.cell, year=e.year, day=e.day, substep=e.substep,
+                    value=e.value)
+
+    def get_annual(self) -> np.ndarray:
+        out = np.empty((12 + self.L, self.ncell), dtype=np.float32)
+        _check(self._lib.h9g_get_annual(self._h, _fp(out)), "h9g_get_annual")
+        return out
+
+    def get_diagnostics(self, dev_ptr: int | None = None) -> np.ndarray:
+        out = np.empty(NDIAG, dtype=np.float64)
+        _check(self._lib.h9g_get_diagnostics(self._h, out.ctypes.data_as(_DP),
+                                             C.c_void_p(dev_ptr) if dev_ptr else None),
+               "h9g_get_diagnostics")
+        return out
+
+    def last_kernel_ms(self) -> float:
+        return float(self._lib.h9g_last_kernel_ms(self._h))
+
+    def total_kernel_ms(self, reset: bool = False) -> float:
+        return float(self._lib.h9g_total_kernel_ms(self._h, int(reset)))
+
+    def kernel_name(self) -> str:
+        return self._lib.h9g_kernel_name(self._h).decode()
+
+
+def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=True,
+        state0: np.ndarray | None = None, device=0):
+    """Run ``nyears`` years from ``year0`` for every cell (HYBRID9.f90:120-290).
+
+    Same contract as ``oracle.port.run`` / ``oracle.refcase.run_case``:
+    forcing is (7, ndays_total, ncell); returns dict(annual (nyears, 12+L,
+    ncell), state (packed), rc, err)."""
+    L = params["theta_s"].shape[1]
+    n = params["fmax"].size
+    with Context(n, zi, nlayers=L, nisurf=nisurf, grow_on=grow_on, device=device) as ctx:
+        ctx.set_params(params)
+        if state0 is None:
+            ctx.init_state()
+        else:
+            ctx.set_state(state0)
+        ann = np.full((nyears, 12 + L, n), np.nan, dtype=np.float32)
+        d0, rc, err = 0, 0, None
+        for y in range(nyears):
+            nt = days_in_year(year0 + y)
+            ctx.push_forcing(y % 2, forcing[:, d0:d0 + nt, :])
+            ctx.run_year(y % 2, year0 + y)
+            rc = ctx.sync(raise_on_stop=False)
+            ann[y] = ctx.get_annual()
+            d0 += nt
+            if rc:
+                err = ctx.last_error()
+                break
+        return dict(annual=ann, state=ctx.get_state(), rc=rc, err=err)

@@ -1,0 +1,60 @@
+"""Build the gfx950 HIP library ``hybrid9_amd/lib/libh9g.so`` in-tree.
+
+``python -m hybrid9_amd.build`` (also called by ``__graft_entry__.build()``).
+hipcc cross-compiles for gfx950 without a GPU.  Numerics flags are part of
+the parity contract: ``-ffp-contract=off`` (the reference executes no FMA;
+h9_math.h issues its FMAs explicitly) and HIP's default correctly-rounded
+f32 division/sqrt and f32 denormal support are kept (no fast-math).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+SRC = HERE / "csrc" / "h9g.hip"
+DEPS = [SRC, HERE / "csrc" / "h9_math.h", HERE / "csrc" / "h9g_step.h",
+        HERE / "csrc" / "h9g_synth.h", HERE.parent / "include" / "h9g.h"]
+OUT = HERE / "lib" / "libh9g.so"
+ARCH = os.environ.get("H9G_ARCH", "gfx950")
+
+FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+         "-fhip-fp32-correctly-rounded-divide-sqrt", "-fPIC", "-shared",
+         "-Wall", "-Wno-unused-value"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and Path(c).exists():
+            return c
+    raise FileNotFoundError("hipcc not found")
+
+
+def up_to_date() -> bool:
+    if not OUT.exists():
+        return False
+    t = OUT.stat().st_mtime
+    return all(d.stat().st_mtime <= t for d in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False, extra=()) -> Path:
+    if not force and up_to_date():
+        return OUT
+    OUT.parent.mkdir(parents=True, exist_ok=True)
+    tmp = OUT.with_suffix(".so.tmp")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *extra, str(SRC), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed:\n{r.stderr[-4000:]}")
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    p = build(force="--force" in sys.argv, verbose=True)
+    print(p)

@@ -1,0 +1,797 @@
+// h9g.hip -- MI355X (gfx950) implementation of the HYBRID9 per-cell
+// time-stepping hot path behind the C-ABI of include/h9g.h.
+//
+// Kernel design:
+//   * h9g_year_kernel<L>: one lane = one soil column.  A launch runs one
+//     calendar year: all days x NISURF substeps of HYDROLOGY plus the daily
+//     GROW, with the whole column state, the soil parameters and the annual
+//     sums held in VGPRs.  HBM traffic per cell-day is the 7 forcing values
+//     (coalesced, cell-fastest) -- the SHARED-state contract of each
+//     substep (376 B at L=8) never leaves the register file.
+//   * glibc-exact expf/powf (h9_math.h) read their 32+16-entry tables from
+//     LDS (per-lane indices, no scalar-cache serialisation).
+//   * no MFMA: nothing here is GEMM-shaped.
+//   * h9g_diag_kernel: deterministic FP64 reduction of global diagnostics
+//     (the payload of the cross-GPU all-reduce).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/h9g.h"
+#include "h9_math.h"
+#include "h9g_step.h"
+#include "h9g_synth.h"
+
+using namespace h9k;
+
+__constant__ uint64_t c_exp2tab[32] = H9M_EXP2F_TAB_INIT;
+__constant__ double c_log2tab[32] = H9M_POWF_LOG2_TAB_INIT;
+static const uint64_t h_exp2tab[32] = H9M_EXP2F_TAB_INIT;
+static const double h_log2tab[32] = H9M_POWF_LOG2_TAB_INIT;
+
+#define H9G_BLOCK 256
+#define NEVT 64
+
+// ---------------------------------------------------------------------------
+// kernel arguments
+// ---------------------------------------------------------------------------
+struct KArgs {
+  int ncell;
+  int nt;          // days in the year
+  int nisurf;
+  int grow_on;
+  size_t fvar;     // forcing variable stride (floats) = max_days * ncell
+  const float *__restrict__ par;   // (4L+1) rows x ncell
+  float *__restrict__ st;          // (4L+9) rows x ncell
+  const float *__restrict__ forc;  // 7 x max_days x ncell (slot base)
+  float *__restrict__ annual;      // (12+L) rows x ncell
+  int *__restrict__ err;           // 4 rows x ncell: code, day, substep, value bits
+  int *__restrict__ err_flag;
+};
+
+__device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
+  const int t = threadIdx.x;
+  if (t < 32) {
+    e2[t] = c_exp2tab[t];
+    l2[t] = c_log2tab[t];
+  }
+  __syncthreads();
+}
+
+template <int L>
+__global__ void __launch_bounds__(H9G_BLOCK) h9g_year_kernel(const KArgs a, const Geo<L> g) {
+  __shared__ uint64_t s_e2[32];
+  __shared__ double s_l2[32];
+  load_tabs(s_e2, s_l2);
+  const h9m::Tabs T = {s_e2, s_l2};
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.ncell) return;
+  const int n = a.ncell;
+
+  Par<L> p;
+  St<L> s;
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    p.ts[i] = a.par[(size_t)(0 * L + i - 1) * n + c];
+    p.hks[i] = a.par[(size_t)(1 * L + i - 1) * n + c];
+    p.bsw[i] = a.par[(size_t)(2 * L + i - 1) * n + c];
+    p.psi[i] = a.par[(size_t)(3 * L + i - 1) * n + c];
+    s.h2o[i] = a.st[(size_t)(0 * L + i - 1) * n + c];
+    s.smp[i] = a.st[(size_t)(2 * L + i - 1) * n + c];
+    s.rootr[i] = a.st[(size_t)(3 * L + i - 1) * n + c];
+  }
+  p.fmax = a.par[(size_t)(4 * L) * n + c];
+  const size_t o8 = (size_t)(4 * L + 1) * n + c;
+  s.zwt = a.st[o8 + 0 * (size_t)n];
+  s.wa = a.st[o8 + 1 * (size_t)n];
+  s.LAI = a.st[o8 + 2 * (size_t)n];
+  s.LAI_litter = a.st[o8 + 3 * (size_t)n];
+  s.pm = a.st[o8 + 4 * (size_t)n];
+  s.pfm = a.st[o8 + 5 * (size_t)n];
+  s.plen = a.st[o8 + 6 * (size_t)n];
+  s.rdepth = a.st[o8 + 7 * (size_t)n];
+
+  // soil mask (HYBRID9.f90:122-123): SUM(theta_s) > trunc
+  float ts_sum = zero;
+#pragma unroll
+  for (int i = 1; i <= L; i++) ts_sum = ts_sum + p.ts[i];
+  if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
+#pragma unroll
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + c] = __builtin_nanf("");
+    return;
+  }
+
+  float npp_sum = zero, plant_mass_sum = zero, rnf_sum = zero;
+  float tas_sum = zero, rlds_sum = zero, rsds_sum = zero, huss_sum = zero;
+  float ps_sum = zero, pr_sum = zero, rhs_sum = zero, h2osoi_sum_total = zero;
+  float theta_sum[L + 1], theta[L + 1];
+#pragma unroll
+  for (int i = 1; i <= L; i++) { theta_sum[i] = zero; theta[i] = zero; }
+  float npp = zero;
+  int code = 0, eday = 0, estep = 0;
+  float errval = 0.0f;
+
+  const float *f = a.forc + c;
+  for (int day = 0; day < a.nt; day++) {
+    const size_t fo = (size_t)day * n;
+    const float tas = f[fo + 0 * a.fvar];
+    const float rlds = f[fo + 1 * a.fvar];
+    const float rsds = f[fo + 2 * a.fvar];
+    const float huss = f[fo + 3 * a.fvar];
+    const float ps = f[fo + 4 * a.fvar];
+    const float pr = f[fo + 5 * a.fvar];
+    const float rhs = f[fo + 6 * a.fvar];
+    Day d;                                        // HYBRID9.f90:168-184
+    d.tak = tas;
+    d.rh = rhs;
+    d.Rnet = 0.92f * rsds + rlds - stbo * (tas * (tas * (tas * tas)));
+    d.PAR = 0.92f * rsds * 2.3f;
+    d.forc_rain = 1.0E3f * pr / rhow;
+    d.lamb = ((2503.0f - 2.386f * (d.tak - tf))) * 1.0E3f;
+    d.huss = huss;
+    d.ps = ps;
+    for (int ns = 0; ns < a.nisurf; ns++) {       // HYBRID9.f90:193-211
+      code = hydrology_step<L>(g, p, d, s, theta, rnf_sum, errval, T);
+      if (code) { eday = day; estep = ns; break; }
+    }
+    if (code) break;
+    if (a.grow_on) grow_day<L>(g, tas, s, npp, T);  // HYBRID9.f90:217
+    tas_sum = tas_sum + tas;                         // :235-254
+    rlds_sum = rlds_sum + rlds;
+    rsds_sum = rsds_sum + rsds;
+    huss_sum = huss_sum + huss;
+    ps_sum = ps_sum + ps;
+    pr_sum = pr_sum + pr;
+    rhs_sum = rhs_sum + rhs;
+    plant_mass_sum = plant_mass_sum + s.pm;
+    npp_sum = npp_sum + npp;
+#pragma unroll
+    for (int i = 1; i <= L; i++) {
+      theta_sum[i] = theta_sum[i] + theta[i];
+      h2osoi_sum_total = h2osoi_sum_total + s.h2o[i];
+    }
+  }
+
+  // state write-back
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    a.st[(size_t)(0 * L + i - 1) * n + c] = s.h2o[i];
+    a.st[(size_t)(2 * L + i - 1) * n + c] = s.smp[i];
+    if (a.grow_on) a.st[(size_t)(3 * L + i - 1) * n + c] = s.rootr[i];
+  }
+  if (a.grow_on) a.st[(size_t)(4 * L) * n + c] = zero;   // rootr_col(Nlevgrnd)
+  a.st[o8 + 0 * (size_t)n] = s.zwt;
+  a.st[o8 + 1 * (size_t)n] = s.wa;
+  a.st[o8 + 2 * (size_t)n] = s.LAI;
+  a.st[o8 + 3 * (size_t)n] = s.LAI_litter;
+  a.st[o8 + 4 * (size_t)n] = s.pm;
+  a.st[o8 + 5 * (size_t)n] = s.pfm;
+  a.st[o8 + 6 * (size_t)n] = s.plen;
+  a.st[o8 + 7 * (size_t)n] = s.rdepth;
+
+  if (code) {
+    a.err[0 * (size_t)n + c] = code;
+    a.err[1 * (size_t)n + c] = eday;
+    a.err[2 * (size_t)n + c] = estep;
+    a.err[3 * (size_t)n + c] = __builtin_bit_cast(int, errval);
+    atomicOr(a.err_flag, 1);
+#pragma unroll
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + c] = __builtin_nanf("");
+    return;
+  }
+  // annual means (HYBRID9.f90:263-290)
+  const int nt = a.nt;
+  float *an = a.annual + c;
+  an[0 * (size_t)n] = npp_sum;
+  an[1 * (size_t)n] = plant_mass_sum / (float)nt;
+  an[2 * (size_t)n] = rnf_sum / (float)(nt * a.nisurf);
+  an[3 * (size_t)n] = zero / (float)(nt * a.nisurf);   // evap_sum is never accumulated
+  an[4 * (size_t)n] = tas_sum / (float)nt;
+  an[5 * (size_t)n] = rlds_sum / (float)nt;
+  an[6 * (size_t)n] = rsds_sum / (float)nt;
+  an[7 * (size_t)n] = huss_sum / (float)nt;
+  an[8 * (size_t)n] = ps_sum / (float)nt;
+  an[9 * (size_t)n] = pr_sum / (float)nt;
+  an[10 * (size_t)n] = rhs_sum / (float)nt;
+#pragma unroll
+  for (int i = 1; i <= L; i++) an[(size_t)(10 + i) * n] = theta_sum[i] / (float)nt;
+  an[(size_t)(11 + L) * n] = h2osoi_sum_total / (float)nt;
+}
+
+template <int L>
+__global__ void __launch_bounds__(H9G_BLOCK) h9g_init_kernel(int ncell, const float *__restrict__ par,
+                                                             float *__restrict__ st, const Geo<L> g) {
+  __shared__ uint64_t s_e2[32];
+  __shared__ double s_l2[32];
+  load_tabs(s_e2, s_l2);
+  const h9m::Tabs T = {s_e2, s_l2};
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncell) return;
+  const int n = ncell;
+  Par<L> p;
+  St<L> s;
+  float h2o_ma[L + 1];
+#pragma unroll
+  for (int i = 1; i <= L; i++) p.ts[i] = par[(size_t)(i - 1) * n + c];
+  init_cell<L>(g, p, s, h2o_ma, T);
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    st[(size_t)(0 * L + i - 1) * n + c] = s.h2o[i];
+    st[(size_t)(1 * L + i - 1) * n + c] = h2o_ma[i];
+    st[(size_t)(2 * L + i - 1) * n + c] = s.smp[i];
+    st[(size_t)(3 * L + i - 1) * n + c] = s.rootr[i];
+  }
+  st[(size_t)(4 * L) * n + c] = zero;
+  const size_t o8 = (size_t)(4 * L + 1) * n + c;
+  st[o8 + 0 * (size_t)n] = s.zwt;
+  st[o8 + 1 * (size_t)n] = s.wa;
+  st[o8 + 2 * (size_t)n] = s.LAI;
+  st[o8 + 3 * (size_t)n] = s.LAI_litter;
+  st[o8 + 4 * (size_t)n] = s.pm;
+  st[o8 + 5 * (size_t)n] = s.pfm;
+  st[o8 + 6 * (size_t)n] = s.plen;
+  st[o8 + 7 * (size_t)n] = s.rdepth;
+}
+
+// deterministic FP64 diagnostics: one block, fixed strided order + tree
+__global__ void __launch_bounds__(1024) h9g_diag_kernel(int ncell, int L, const float *__restrict__ annual,
+                                                        const float *__restrict__ st,
+                                                        const int *__restrict__ err, double *__restrict__ out) {
+  __shared__ double red[1024];
+  double acc[H9G_NDIAG];
+  for (int k = 0; k < H9G_NDIAG; k++) acc[k] = 0.0;
+  const size_t n = ncell;
+  const size_t o8 = (size_t)(4 * L + 1) * n;
+  for (int c = threadIdx.x; c < ncell; c += blockDim.x) {
+    const float rnf = annual[2 * n + c];
+    if (err[c] != 0) { acc[11] += 1.0; continue; }
+    if (rnf != rnf) continue;                    // non-soil cell
+    acc[0] += 1.0;
+    acc[1] += (double)rnf;
+    acc[2] += (double)annual[(size_t)(11 + L) * n + c];
+    acc[3] += (double)st[o8 + 0 * n + c];
+    acc[4] += (double)st[o8 + 1 * n + c];
+    acc[5] += (double)annual[0 * n + c];
+    acc[6] += (double)annual[1 * n + c];
+    acc[7] += (double)st[o8 + 2 * n + c];
+    acc[8] += (double)annual[11 * n + c];
+    acc[9] += (double)annual[4 * n + c];
+    acc[10] += (double)annual[9 * n + c];
+  }
+  for (int k = 0; k < H9G_NDIAG; k++) {
+    red[threadIdx.x] = acc[k];
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[k] = red[0];
+    __syncthreads();
+  }
+}
+
+template <int L>
+__global__ void __launch_bounds__(H9G_BLOCK) h9g_synth_params_kernel(int ncell, const int64_t *__restrict__ gid,
+                                                                     uint64_t seed, float *__restrict__ par) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncell) return;
+  const size_t n = ncell;
+  const uint64_t g = (uint64_t)gid[c];
+#pragma unroll
+  for (int l = 0; l < L; l++) {
+    float ts, hk, b, ps;
+    h9s::params(seed, g, l, &ts, &hk, &b, &ps);
+    par[(size_t)(0 * L + l) * n + c] = ts;
+    par[(size_t)(1 * L + l) * n + c] = hk;
+    par[(size_t)(2 * L + l) * n + c] = b;
+    par[(size_t)(3 * L + l) * n + c] = ps;
+  }
+  par[(size_t)(4 * L) * n + c] = h9s::fmax_param(seed, g);
+}
+
+__global__ void __launch_bounds__(H9G_BLOCK) h9g_synth_forcing_kernel(int ncell, int nday, int day0,
+                                                                      const int64_t *__restrict__ gid,
+                                                                      const float *__restrict__ lat, uint64_t seed,
+                                                                      size_t fvar, float *__restrict__ forc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int d = blockIdx.y;
+  if (c >= ncell || d >= nday) return;
+  float v[7];
+  h9s::forcing(seed, (uint64_t)gid[c], lat[c], (int64_t)day0 + d, v);
+#pragma unroll
+  for (int k = 0; k < 7; k++) forc[k * fvar + (size_t)d * ncell + c] = v[k];
+}
+
+__global__ void h9g_math_kernel(int n, const float *x, const float *y, float *out) {
+  __shared__ uint64_t s_e2[32];
+  __shared__ double s_l2[32];
+  load_tabs(s_e2, s_l2);
+  const h9m::Tabs T = {s_e2, s_l2};
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = y ? h9m::powf(x[i], y[i], T) : h9m::expf(x[i], T);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct h9g_ctx {
+  h9g_config cfg;
+  int device = 0;
+  int L = 8;
+  size_t n = 0;
+  hipStream_t sc = nullptr, sx = nullptr;      // compute, copy
+  float *d_par = nullptr, *d_st = nullptr, *d_forc = nullptr, *d_ann = nullptr;
+  int *d_err = nullptr, *d_errflag = nullptr;
+  double *d_diag = nullptr;
+  int64_t *d_gid = nullptr;
+  float *d_lat = nullptr;
+  std::vector<int> slot_days;
+  std::vector<hipEvent_t> ev_copied, ev_consumed;
+  hipEvent_t ev0[NEVT], ev1[NEVT];
+  int nev = 0;
+  float last_ms = 0.0f;
+  double total_ms = 0.0;
+  int last_year = 0;
+  int params_set = 0, state_set = 0, ran = 0;
+  h9g_error last_err{};
+  const char *kname = "";
+};
+
+#define HIPCHK(x)                                                              \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "h9g: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), \
+              __FILE__, __LINE__);                                             \
+      return H9G_EHIP;                                                         \
+    }                                                                          \
+  } while (0)
+
+static int days_in_year(int y) {   // INIT.f90:844-859
+  if (y % 4 != 0) return 365;
+  if (y % 100 != 0) return 366;
+  if (y % 400 != 0) return 365;
+  return 366;
+}
+
+template <int L>
+static Geo<L> make_geo(const h9g_config &c) {
+  Geo<L> g;
+  for (int i = 0; i <= L + 1; i++) g.zi[i] = c.zi[i];
+  for (int i = 1; i <= L; i++) g.dz[i] = g.zi[i] - g.zi[i - 1];
+  for (int i = 1; i <= L; i++) g.zc[i] = g.zi[i] - g.dz[i] / 2.0f;
+  for (int i = 1; i <= L; i++) g.zi_m[i] = g.zi[i] / 1000.0f;
+  g.dz[0] = g.zc[0] = g.zi_m[0] = 0.0f;
+  g.dt = 86400.0f / (float)c.nisurf;              // INIT.f90:214
+  return g;
+}
+
+static unsigned nblocks(size_t n) { return (unsigned)((n + H9G_BLOCK - 1) / H9G_BLOCK); }
+
+extern "C" {
+
+int h9g_abi_version(void) { return H9G_ABI_VERSION; }
+
+int h9g_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int h9g_state_size(int nlayers) { return 4 * nlayers + 9; }
+
+void h9g_destroy(h9g_ctx *ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->sc) hipStreamSynchronize(ctx->sc);
+  if (ctx->sx) hipStreamSynchronize(ctx->sx);
+  (void)hipFree(ctx->d_par);
+  (void)hipFree(ctx->d_st);
+  (void)hipFree(ctx->d_forc);
+  (void)hipFree(ctx->d_ann);
+  (void)hipFree(ctx->d_err);
+  (void)hipFree(ctx->d_errflag);
+  (void)hipFree(ctx->d_diag);
+  (void)hipFree(ctx->d_gid);
+  (void)hipFree(ctx->d_lat);
+  for (auto e : ctx->ev_copied) hipEventDestroy(e);
+  for (auto e : ctx->ev_consumed) hipEventDestroy(e);
+  for (int i = 0; i < NEVT; i++) {
+    (void)hipEventDestroy(ctx->ev0[i]);
+    (void)hipEventDestroy(ctx->ev1[i]);
+  }
+  if (ctx->sc) hipStreamDestroy(ctx->sc);
+  if (ctx->sx) hipStreamDestroy(ctx->sx);
+  delete ctx;
+}
+
+h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
+  if (!cfg || cfg->ncell <= 0 || !(cfg->nlayers == 8 || cfg->nlayers == 10) || cfg->nisurf < 1 ||
+      cfg->max_days < 366 || cfg->nslots < 1 || cfg->nslots > 8)
+    return nullptr;
+  for (int i = 1; i <= cfg->nlayers + 1; i++)
+    if (!(cfg->zi[i] > cfg->zi[i - 1])) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  h9g_ctx *ctx = new h9g_ctx();
+  ctx->cfg = *cfg;
+  ctx->device = device;
+  ctx->L = cfg->nlayers;
+  ctx->n = (size_t)cfg->ncell;
+  const size_t n = ctx->n;
+  const int L = ctx->L;
+  bool ok = hipStreamCreateWithFlags(&ctx->sc, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&ctx->sx, hipStreamNonBlocking) == hipSuccess &&
+            hipMalloc(&ctx->d_par, sizeof(float) * (4 * L + 1) * n) == hipSuccess &&
+            hipMalloc(&ctx->d_st, sizeof(float) * (4 * L + 9) * n) == hipSuccess &&
+            hipMalloc(&ctx->d_forc, sizeof(float) * 7 * (size_t)cfg->max_days * n * cfg->nslots) == hipSuccess &&
+            hipMalloc(&ctx->d_ann, sizeof(float) * (12 + L) * n) == hipSuccess &&
+            hipMalloc(&ctx->d_err, sizeof(int) * 4 * n) == hipSuccess &&
+            hipMalloc(&ctx->d_errflag, sizeof(int)) == hipSuccess &&
+            hipMalloc(&ctx->d_diag, sizeof(double) * H9G_NDIAG) == hipSuccess &&
+            hipMalloc(&ctx->d_gid, sizeof(int64_t) * n) == hipSuccess &&
+            hipMalloc(&ctx->d_lat, sizeof(float) * n) == hipSuccess;
+  if (ok) {
+    ok = hipMemset(ctx->d_err, 0, sizeof(int) * 4 * n) == hipSuccess &&
+         hipMemset(ctx->d_errflag, 0, sizeof(int)) == hipSuccess &&
+         hipMemset(ctx->d_diag, 0, sizeof(double) * H9G_NDIAG) == hipSuccess &&
+         hipMemset(ctx->d_ann, 0xff, sizeof(float) * (12 + L) * n) == hipSuccess;
+  }
+  ctx->slot_days.assign(cfg->nslots, 0);
+  ctx->ev_copied.resize(cfg->nslots);
+  ctx->ev_consumed.resize(cfg->nslots);
+  for (int s = 0; ok && s < cfg->nslots; s++)
+    ok = hipEventCreateWithFlags(&ctx->ev_copied[s], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&ctx->ev_consumed[s], hipEventDisableTiming) == hipSuccess;
+  for (int i = 0; ok && i < NEVT; i++)
+    ok = hipEventCreate(&ctx->ev0[i]) == hipSuccess && hipEventCreate(&ctx->ev1[i]) == hipSuccess;
+  if (!ok) {
+    fprintf(stderr, "h9g_create: device allocation failed (ncell=%d)\n", cfg->ncell);
+    h9g_destroy(ctx);
+    return nullptr;
+  }
+  ctx->kname = (L == 8) ? "h9g_year_kernel<8>" : "h9g_year_kernel<10>";
+  return ctx;
+}
+
+// (L, ncell) layer-fastest host arrays -> device rows
+int h9g_set_params(h9g_ctx *ctx, const float *theta_s, const float *hksat, const float *bsw,
+                   const float *psi_s, const float *fmax) {
+  if (!ctx || !theta_s || !hksat || !bsw || !psi_s || !fmax) return H9G_EINVAL;
+  const size_t n = ctx->n;
+  const int L = ctx->L;
+  std::vector<float> rows((4 * L + 1) * n);
+  const float *src[4] = {theta_s, hksat, bsw, psi_s};
+  for (int k = 0; k < 4; k++)
+    for (size_t c = 0; c < n; c++)
+      for (int i = 0; i < L; i++) rows[(size_t)(k * L + i) * n + c] = src[k][c * L + i];
+  memcpy(&rows[(size_t)(4 * L) * n], fmax, sizeof(float) * n);
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(ctx->d_par, rows.data(), sizeof(float) * rows.size(), hipMemcpyHostToDevice, ctx->sc));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  ctx->params_set = 1;
+  return 0;
+}
+
+int h9g_init_state(h9g_ctx *ctx) {
+  if (!ctx) return H9G_EINVAL;
+  if (!ctx->params_set) return H9G_ESTATE;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int n = (int)ctx->n;
+  if (ctx->L == 8)
+    h9g_init_kernel<8><<<nblocks(n), H9G_BLOCK, 0, ctx->sc>>>(n, ctx->d_par, ctx->d_st, make_geo<8>(ctx->cfg));
+  else
+    h9g_init_kernel<10><<<nblocks(n), H9G_BLOCK, 0, ctx->sc>>>(n, ctx->d_par, ctx->d_st, make_geo<10>(ctx->cfg));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemsetAsync(ctx->d_err, 0, sizeof(int) * 4 * ctx->n, ctx->sc));
+  HIPCHK(hipMemsetAsync(ctx->d_errflag, 0, sizeof(int), ctx->sc));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  ctx->state_set = 1;
+  ctx->last_err = h9g_error{};
+  return 0;
+}
+
+// packed (field-major, width-fastest) <-> device rows
+static void widths(int L, int *w) {
+  const int ws[12] = {L, L, L, L + 1, 1, 1, 1, 1, 1, 1, 1, 1};
+  for (int k = 0; k < 12; k++) w[k] = ws[k];
+}
+
+int h9g_set_state(h9g_ctx *ctx, const float *packed) {
+  if (!ctx || !packed) return H9G_EINVAL;
+  const size_t n = ctx->n;
+  int w[12];
+  widths(ctx->L, w);
+  std::vector<float> rows((size_t)h9g_state_size(ctx->L) * n);
+  size_t off = 0, row = 0;
+  for (int k = 0; k < 12; k++) {
+    for (size_t c = 0; c < n; c++)
+      for (int i = 0; i < w[k]; i++) rows[(row + i) * n + c] = packed[off + c * w[k] + i];
+    off += n * w[k];
+    row += w[k];
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpyAsync(ctx->d_st, rows.data(), sizeof(float) * rows.size(), hipMemcpyHostToDevice, ctx->sc));
+  HIPCHK(hipMemsetAsync(ctx->d_err, 0, sizeof(int) * 4 * n, ctx->sc));
+  HIPCHK(hipMemsetAsync(ctx->d_errflag, 0, sizeof(int), ctx->sc));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  ctx->state_set = 1;
+  ctx->last_err = h9g_error{};
+  return 0;
+}
+
+int h9g_get_state(h9g_ctx *ctx, float *packed) {
+  if (!ctx || !packed) return H9G_EINVAL;
+  const size_t n = ctx->n;
+  int w[12];
+  widths(ctx->L, w);
+  std::vector<float> rows((size_t)h9g_state_size(ctx->L) * n);
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  HIPCHK(hipMemcpy(rows.data(), ctx->d_st, sizeof(float) * rows.size(), hipMemcpyDeviceToHost));
+  size_t off = 0, row = 0;
+  for (int k = 0; k < 12; k++) {
+    for (size_t c = 0; c < n; c++)
+      for (int i = 0; i < w[k]; i++) packed[off + c * w[k] + i] = rows[(row + i) * n + c];
+    off += n * w[k];
+    row += w[k];
+  }
+  return 0;
+}
+
+float *h9g_forcing_slot(h9g_ctx *ctx, int slot) {
+  if (!ctx || slot < 0 || slot >= ctx->cfg.nslots) return nullptr;
+  return ctx->d_forc + (size_t)slot * 7 * ctx->cfg.max_days * ctx->n;
+}
+
+void *h9g_host_alloc(size_t bytes) {
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void h9g_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
+}
+
+// (7, nday, ncell) -> slot (7, max_days, ncell)
+static int push_impl(h9g_ctx *ctx, int slot, int nday, const float *src, hipMemcpyKind kind, bool async) {
+  if (!ctx || !src || slot < 0 || slot >= ctx->cfg.nslots || nday < 1 || nday > ctx->cfg.max_days)
+    return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  float *dst = h9g_forcing_slot(ctx, slot);
+  const size_t n = ctx->n;
+  HIPCHK(hipStreamWaitEvent(ctx->sx, ctx->ev_consumed[slot], 0));
+  HIPCHK(hipMemcpy2DAsync(dst, sizeof(float) * ctx->cfg.max_days * n, src, sizeof(float) * nday * n,
+                          sizeof(float) * nday * n, 7, kind, ctx->sx));
+  HIPCHK(hipEventRecord(ctx->ev_copied[slot], ctx->sx));
+  if (!async) HIPCHK(hipStreamSynchronize(ctx->sx));
+  ctx->slot_days[slot] = nday;
+  return 0;
+}
+
+int h9g_push_forcing(h9g_ctx *ctx, int slot, int nday, const float *forcing, int async) {
+  return push_impl(ctx, slot, nday, forcing, hipMemcpyHostToDevice, async != 0);
+}
+
+int h9g_push_forcing_device(h9g_ctx *ctx, int slot, int nday, const float *dev_forcing) {
+  return push_impl(ctx, slot, nday, dev_forcing, hipMemcpyDeviceToDevice, true);
+}
+
+int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
+  if (!ctx || slot < 0 || slot >= ctx->cfg.nslots || jyear < 1861 || jyear > 2299) return H9G_EINVAL;
+  if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
+  const int nt = days_in_year(jyear);
+  if (ctx->slot_days[slot] < nt) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamWaitEvent(ctx->sc, ctx->ev_copied[slot], 0));
+  KArgs a;
+  a.ncell = (int)ctx->n;
+  a.nt = nt;
+  a.nisurf = ctx->cfg.nisurf;
+  a.grow_on = ctx->cfg.grow_on;
+  a.fvar = (size_t)ctx->cfg.max_days * ctx->n;
+  a.par = ctx->d_par;
+  a.st = ctx->d_st;
+  a.forc = h9g_forcing_slot(ctx, slot);
+  a.annual = ctx->d_ann;
+  a.err = ctx->d_err;
+  a.err_flag = ctx->d_errflag;
+  if (ctx->nev >= NEVT) {   // fold finished timings before reusing events
+    HIPCHK(hipStreamSynchronize(ctx->sc));
+    for (int i = 0; i < ctx->nev; i++) {
+      float ms = 0.0f;
+      (void)hipEventElapsedTime(&ms, ctx->ev0[i], ctx->ev1[i]);
+      ctx->total_ms += ms;
+      ctx->last_ms = ms;
+    }
+    ctx->nev = 0;
+  }
+  const int e = ctx->nev++;
+  HIPCHK(hipEventRecord(ctx->ev0[e], ctx->sc));
+  if (ctx->L == 8)
+    h9g_year_kernel<8><<<nblocks(ctx->n), H9G_BLOCK, 0, ctx->sc>>>(a, make_geo<8>(ctx->cfg));
+  else
+    h9g_year_kernel<10><<<nblocks(ctx->n), H9G_BLOCK, 0, ctx->sc>>>(a, make_geo<10>(ctx->cfg));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ctx->ev1[e], ctx->sc));
+  HIPCHK(hipEventRecord(ctx->ev_consumed[slot], ctx->sc));
+  h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)ctx->n, ctx->L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
+  HIPCHK(hipGetLastError());
+  ctx->last_year = jyear;
+  ctx->ran = 1;
+  return 0;
+}
+
+int h9g_sync(h9g_ctx *ctx) {
+  if (!ctx) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->sx));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  for (int i = 0; i < ctx->nev; i++) {
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0[i], ctx->ev1[i]));
+    ctx->total_ms += ms;
+    ctx->last_ms = ms;
+  }
+  ctx->nev = 0;
+  int flag = 0;
+  HIPCHK(hipMemcpy(&flag, ctx->d_errflag, sizeof(int), hipMemcpyDeviceToHost));
+  if (!flag) return 0;
+  if (ctx->last_err.code == 0) {
+    const size_t n = ctx->n;
+    std::vector<int> e(4 * n);
+    HIPCHK(hipMemcpy(e.data(), ctx->d_err, sizeof(int) * 4 * n, hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < n; c++) {
+      if (e[c]) {        // lowest cell index first, as the reference's cell-outer loop
+        ctx->last_err.code = e[c];
+        ctx->last_err.cell = (int)c;
+        ctx->last_err.year = ctx->last_year;
+        ctx->last_err.day = e[n + c];
+        ctx->last_err.substep = e[2 * n + c];
+        ctx->last_err.value = __builtin_bit_cast(float, e[3 * n + c]);
+        break;
+      }
+    }
+  }
+  return ctx->last_err.code;
+}
+
+int h9g_last_error(h9g_ctx *ctx, h9g_error *err) {
+  if (!ctx || !err) return H9G_EINVAL;
+  *err = ctx->last_err;
+  return 0;
+}
+
+int h9g_get_annual(h9g_ctx *ctx, float *annual) {
+  if (!ctx || !annual) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  HIPCHK(hipMemcpy(annual, ctx->d_ann, sizeof(float) * (12 + ctx->L) * ctx->n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int h9g_get_diagnostics(h9g_ctx *ctx, double *host_out, double *dev_out) {
+  if (!ctx) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (dev_out)
+    HIPCHK(hipMemcpyAsync(dev_out, ctx->d_diag, sizeof(double) * H9G_NDIAG, hipMemcpyDeviceToDevice, ctx->sc));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  if (host_out) HIPCHK(hipMemcpy(host_out, ctx->d_diag, sizeof(double) * H9G_NDIAG, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int h9g_set_cells(h9g_ctx *ctx, const int64_t *gid, const float *lat) {
+  if (!ctx || !gid || !lat) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemcpy(ctx->d_gid, gid, sizeof(int64_t) * ctx->n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(ctx->d_lat, lat, sizeof(float) * ctx->n, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int h9g_synth_params(h9g_ctx *ctx, uint64_t seed) {
+  if (!ctx) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int n = (int)ctx->n;
+  if (ctx->L == 8)
+    h9g_synth_params_kernel<8><<<nblocks(n), H9G_BLOCK, 0, ctx->sc>>>(n, ctx->d_gid, seed, ctx->d_par);
+  else
+    h9g_synth_params_kernel<10><<<nblocks(n), H9G_BLOCK, 0, ctx->sc>>>(n, ctx->d_gid, seed, ctx->d_par);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  ctx->params_set = 1;
+  return 0;
+}
+
+int h9g_synth_forcing(h9g_ctx *ctx, int slot, uint64_t seed, int day0, int nday) {
+  if (!ctx || slot < 0 || slot >= ctx->cfg.nslots || nday < 1 || nday > ctx->cfg.max_days || day0 < 0)
+    return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamWaitEvent(ctx->sx, ctx->ev_consumed[slot], 0));
+  dim3 grid(nblocks(ctx->n), (unsigned)nday);
+  h9g_synth_forcing_kernel<<<grid, H9G_BLOCK, 0, ctx->sx>>>((int)ctx->n, nday, day0, ctx->d_gid, ctx->d_lat, seed,
+                                                           (size_t)ctx->cfg.max_days * ctx->n,
+                                                           h9g_forcing_slot(ctx, slot));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ctx->ev_copied[slot], ctx->sx));
+  ctx->slot_days[slot] = nday;
+  return 0;
+}
+
+float h9g_last_kernel_ms(h9g_ctx *ctx) { return ctx ? ctx->last_ms : 0.0f; }
+
+double h9g_total_kernel_ms(h9g_ctx *ctx, int reset) {
+  if (!ctx) return 0.0;
+  const double t = ctx->total_ms;
+  if (reset) ctx->total_ms = 0.0;
+  return t;
+}
+
+const char *h9g_kernel_name(h9g_ctx *ctx) { return ctx ? ctx->kname : ""; }
+
+int h9g_math_selftest(int device, int n, const float *x, const float *y, float *out) {
+  if (n <= 0 || !x || !out) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(device));
+  float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  HIPCHK(hipMalloc(&dx, sizeof(float) * n));
+  HIPCHK(hipMalloc(&dout, sizeof(float) * n));
+  HIPCHK(hipMemcpy(dx, x, sizeof(float) * n, hipMemcpyHostToDevice));
+  if (y) {
+    HIPCHK(hipMalloc(&dy, sizeof(float) * n));
+    HIPCHK(hipMemcpy(dy, y, sizeof(float) * n, hipMemcpyHostToDevice));
+  }
+  h9g_math_kernel<<<(n + 255) / 256, 256>>>(n, dx, dy, dout);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, sizeof(float) * n, hipMemcpyDeviceToHost));
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  (void)hipFree(dout);
+  return 0;
+}
+
+// Host build of the synthetic generator (CPU tests pin it to synth.py).
+int h9g_synth_host(uint64_t seed, int nlayers, int ncell, const int64_t *gid, const float *lat, int day0,
+                   int nday, float *params_out, float *forcing_out) {
+  if (ncell < 0 || nlayers < 1 || nlayers > H9G_LMAX) return H9G_EINVAL;
+  const size_t n = ncell;
+  const int L = nlayers;
+  if (params_out) {
+    for (size_t c = 0; c < n; c++) {
+      for (int l = 0; l < L; l++) {
+        float ts, hk, b, ps;
+        h9s::params(seed, (uint64_t)gid[c], l, &ts, &hk, &b, &ps);
+        params_out[0 * n * L + c * L + l] = ts;
+        params_out[1 * n * L + c * L + l] = hk;
+        params_out[2 * n * L + c * L + l] = b;
+        params_out[3 * n * L + c * L + l] = ps;
+      }
+      params_out[4 * n * L + c] = h9s::fmax_param(seed, (uint64_t)gid[c]);
+    }
+  }
+  if (forcing_out) {
+    for (int d = 0; d < nday; d++)
+      for (size_t c = 0; c < n; c++) {
+        float v[7];
+        h9s::forcing(seed, (uint64_t)gid[c], lat[c], (int64_t)day0 + d, v);
+        for (int k = 0; k < 7; k++) forcing_out[(size_t)k * nday * n + (size_t)d * n + c] = v[k];
+      }
+  }
+  return 0;
+}
+
+// Host build of the device math, for CPU checks of the shipped object.
+float h9g_host_expf(float x) {
+  const h9m::Tabs T = {h_exp2tab, h_log2tab};
+  return h9m::expf(x, T);
+}
+float h9g_host_powf(float x, float y) {
+  const h9m::Tabs T = {h_exp2tab, h_log2tab};
+  return h9m::powf(x, y, T);
+}
+
+}  // extern "C"

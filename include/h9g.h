@@ -1,0 +1,156 @@
+/*
+ * h9g.h -- C-ABI of the MI355X HYBRID9 hot path (libh9g.so).
+ *
+ * Replaces the PGF cell loop of the reference driver
+ *   /root/reference/SOURCE/HYBRID9.f90:120-295   (cell -> year -> day ->
+ *   substep loop calling HYDROLOGY at :203 and GROW at :217)
+ * which has no plugin/FFI surface of its own: HYDROLOGY and GROW take no
+ * arguments and communicate through MODULE SHARED / CONTROL globals
+ * (/root/reference/SOURCE/HYDROLOGY.f90:10-11, GROW.f90:11-12).  One call
+ * of h9g_run_year advances every cell of a context through one calendar
+ * year, exactly as one pass of HYBRID9.f90:130-291 does for one cell.
+ *
+ * Plain pointers and sizes only.  Host arrays use the reference's
+ * Fortran layouts (SHARED.f90), with the land cells of a block compacted
+ * into one dimension:
+ *   per-layer arrays   A(L, ncell)     layer fastest   (SHARED.f90:398-429)
+ *   per-cell arrays    A(ncell)                        (SHARED.f90:446-472)
+ *   forcing            F(ncell, nday)  cell fastest, one array per variable
+ *                      in READ_PGF.f90 order: tas rlds rsds huss ps pr rhs
+ * The fortran/h9_gpu.f90 module binds every entry point with BIND(C).
+ *
+ * Semantics: bit-identical to the reference for isolated cells (every cell
+ * carries its own hidden matric potential smp, SHARED.f90:198).
+ * Threading: one host thread per context; contexts are not re-entrant;
+ * one context per GPU.  All calls return 0 on success, a positive
+ * H9G_ERR_* code for a reference STOP condition (details via
+ * h9g_last_error) or a negative H9G_E* code for API/HIP failures.
+ */
+#ifndef H9G_H
+#define H9G_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define H9G_ABI_VERSION 1
+#define H9G_LMAX 10          /* soil layers supported: 8 (reference) or 10 */
+#define H9G_NFORCING 7
+#define H9G_NANNUAL_SCALARS 11
+#define H9G_NDIAG 12
+
+/* reference STOP sites (HYDROLOGY.f90) */
+#define H9G_ERR_TRIDIAG1 1   /* :806-812  bmx(1) == 0            */
+#define H9G_ERR_TRIDIAG2 2   /* :818-825  zero pivot             */
+#define H9G_ERR_RSUB_POS 3   /* :1068-1072 rsub_top_tot > 0      */
+#define H9G_ERR_IMBALANCE 4  /* :1244-1274 |w1 - w0| > 0.1 mm    */
+/* API / runtime failures */
+#define H9G_EINVAL (-1)
+#define H9G_EHIP (-2)
+#define H9G_ENOMEM (-3)
+#define H9G_ESTATE (-4)
+
+typedef struct h9g_ctx h9g_ctx;
+
+typedef struct {
+  int32_t ncell;       /* land cells owned by this context (shard)          */
+  int32_t nlayers;     /* L: 8 or 10 (SHARED.f90:294 nsoil_layers_max)      */
+  int32_t nisurf;      /* substeps per day (driver.txt line 2, INIT.f90:183) */
+  int32_t grow_on;     /* 1: CALL GROW daily (HYBRID9.f90:217); 0: frozen   */
+  int32_t max_days;    /* forcing slot capacity in days (>= 366)            */
+  int32_t nslots;      /* forcing slots (2 = double-buffered prefetch)      */
+  float zi[H9G_LMAX + 2]; /* zi(0:L+1) mm (driver.txt:17-26, INIT.f90:202)  */
+} h9g_config;
+
+typedef struct {
+  int32_t code;        /* H9G_ERR_* of the first failing cell (0: none)     */
+  int32_t cell;        /* its 0-based index in the context                  */
+  int32_t year;        /* calendar year                                     */
+  int32_t day;         /* 0-based day of year (DOY-1)                       */
+  int32_t substep;     /* 0-based NS-1                                      */
+  float value;         /* w1-w0, pivot row, rsub_top_tot ...               */
+} h9g_error;
+
+/* --- lifetime -------------------------------------------------------- */
+int h9g_abi_version(void);
+int h9g_device_count(void);
+/* Creates a context on HIP device `device`; NULL on failure. */
+h9g_ctx *h9g_create(const h9g_config *cfg, int device);
+void h9g_destroy(h9g_ctx *ctx);
+
+/* --- parameters and state (INIT.f90) ---------------------------------- */
+/* theta_s, hksat, bsw, psi_s: (L, ncell); fmax: (ncell).  Units after
+ * INIT.f90:611-631 (mm^3/mm^3, mm/s, -, mm). */
+int h9g_set_params(h9g_ctx *ctx, const float *theta_s, const float *hksat,
+                   const float *bsw, const float *psi_s, const float *fmax);
+/* Initial state of INIT.f90:707-811 for every cell (smp = 0). */
+int h9g_init_state(h9g_ctx *ctx);
+/* Packed per-cell state, fields in this order, each (width, ncell) with
+ * width-fastest:  h2osoi_liq(L) h2osoi_liq_ma(L) smp(L) rootr_col(L+1)
+ * zwt wa LAI LAI_litter plant_mass plant_foliage_mass plant_length rdepth
+ * -> h9g_state_size(L) = 4L+9 floats per cell. */
+int h9g_state_size(int nlayers);
+int h9g_set_state(h9g_ctx *ctx, const float *packed);
+int h9g_get_state(h9g_ctx *ctx, float *packed);
+
+/* --- forcing (READ_PGF.f90) ------------------------------------------ */
+/* Copies nday days of forcing, 7 arrays of (ncell, nday) stacked as
+ * (7, nday, ncell), into slot `slot`.  async=1 enqueues the copy on the
+ * context's copy stream (host memory should be pinned, see
+ * h9g_host_alloc); h9g_run_year orders itself after it. */
+int h9g_push_forcing(h9g_ctx *ctx, int slot, int nday, const float *forcing,
+                     int async);
+/* Same from device memory (e.g. a slab already resident in HBM). */
+int h9g_push_forcing_device(h9g_ctx *ctx, int slot, int nday,
+                            const float *dev_forcing);
+/* Device pointer of a slot (capacity max_days), for zero-copy producers. */
+float *h9g_forcing_slot(h9g_ctx *ctx, int slot);
+void *h9g_host_alloc(size_t bytes);   /* pinned host memory */
+void h9g_host_free(void *p);
+
+/* --- the hot path ----------------------------------------------------- */
+/* Advance every cell through calendar year `jyear` (365/366 days by
+ * INIT.f90:844-859) using the forcing in `slot` starting at its day 0.
+ * Enqueued on the compute stream; returns after launch.  Errors are
+ * reported by the next h9g_sync. */
+int h9g_run_year(h9g_ctx *ctx, int slot, int jyear);
+/* Wait for all work; returns the first STOP code raised, if any. */
+int h9g_sync(h9g_ctx *ctx);
+int h9g_last_error(h9g_ctx *ctx, h9g_error *err);
+
+/* --- outputs (HYBRID9.f90:263-290) ------------------------------------ */
+/* Annual means of the last year run, (12+L) rows of (ncell):
+ * npp plant_mass rnf evap tas rlds rsds huss ps pr rhs theta(1..L)
+ * theta_total  (axy_* of SHARED.f90:478-493, NaN for failed cells). */
+int h9g_get_annual(h9g_ctx *ctx, float *annual);
+/* Global diagnostics of the last year (FP64 sums over this context's
+ * cells, deterministic order): see H9G_DIAG_* in DESIGN.md.  Intended
+ * for an all-reduce across GPUs.  dev_out (may be NULL) receives a
+ * device-side copy; host_out (may be NULL) a host copy. */
+int h9g_get_diagnostics(h9g_ctx *ctx, double *host_out, double *dev_out);
+
+/* --- synthetic inputs (hybrid9_amd/synth.py, bit-identical) ----------- */
+/* Cells are identified by their grid id (iy*nx+ix) and latitude. */
+int h9g_set_cells(h9g_ctx *ctx, const int64_t *gid, const float *lat);
+int h9g_synth_params(h9g_ctx *ctx, uint64_t seed);
+int h9g_synth_forcing(h9g_ctx *ctx, int slot, uint64_t seed, int day0,
+                      int nday);
+
+/* --- measurement ------------------------------------------------------ */
+/* Device time (HIP events on the compute stream) of the last year kernel,
+ * and of all year kernels since the last reset. */
+float h9g_last_kernel_ms(h9g_ctx *ctx);
+double h9g_total_kernel_ms(h9g_ctx *ctx, int reset);
+const char *h9g_kernel_name(h9g_ctx *ctx);
+
+/* --- self test of the device math (h9_math.h vs glibc) ---------------- */
+/* out[i] = expf(x[i]) if y == NULL, else powf(x[i], y[i]), on device. */
+int h9g_math_selftest(int device, int n, const float *x, const float *y,
+                      float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* H9G_H */

@@ -136,6 +136,14 @@ ALLOCATE (rdepth (nplants_max,lon_c,lat_c))
 ALLOCATE (nplants (lon_c,lat_c), LAI (lon_c,lat_c), LAI_litter (lon_c,lat_c))
 ALLOCATE (rootr_col (1:Nlevgrnd,lon_c,lat_c))
 ALLOCATE (Fmax (lon_c,lat_c))
+! lon/lat are only printed by the reference's STOP diagnostics
+! (HYDROLOGY.f90:810,823,1250): cell index and 0 here.
+ALLOCATE (lon (lon_c), lat (lat_c))
+DO I = 1, lon_c
+  lon (I) = FLOAT (I)
+END DO
+lat = zero
+my_id = 0
 ALLOCATE (h2osoi_liq (L,lon_c,lat_c), h2osoi_liq_ma (L,lon_c,lat_c))
 ALLOCATE (zwt (lon_c,lat_c), wa (lon_c,lat_c))
 ALLOCATE (theta_s (L,lon_c,lat_c), theta_ma_s (L,lon_c,lat_c))

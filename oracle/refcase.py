@@ -84,12 +84,45 @@ def write_case(d, *, zi, params, forcing, nisurf=48, year0=1901, nyears=1,
         pack_state(state0, L).tofile(d / "state0.f32")
 
 
+class RefStop(RuntimeError):
+    """The reference executed one of its STOP statements (HYDROLOGY.f90)."""
+
+    def __init__(self, stdout: str):
+        self.stdout = stdout
+        self.info = parse_stop(stdout)
+        super().__init__(f"reference STOP: {self.info}")
+
+
+def parse_stop(out: str) -> dict:
+    """Fields printed by HYDROLOGY.f90:806-825 / 1068-1072 / 1245-1273."""
+    info = {}
+    lines = out.splitlines()
+    for i, ln in enumerate(lines):
+        t = ln.strip()
+        if t.startswith("Water imbalance > 0.1 mm"):
+            info["code"] = 4
+            info["value"] = float(t.split()[-1])
+        elif t.startswith("Problem with tridiagonal 1."):
+            info["code"] = 1
+        elif t.startswith("Problem with tridiagonal 2."):
+            info["code"] = 2
+        elif t.startswith("rsub_top_tot is positive"):
+            info["code"] = 3
+        elif t.startswith("DiTIME ="):
+            info["day"] = int(t.split("=")[1]) - 1          # 0-based day of the year
+        elif t.startswith("my_id x y"):
+            info["cell"] = int(t.split()[-2]) - 1           # 0-based cell
+    return info
+
+
 def run_ref(d, timeout=3600):
     if not REF_BIN.exists():
         raise FileNotFoundError(f"{REF_BIN} missing: run `make -C oracle ref`")
     r = subprocess.run([str(REF_BIN), str(d)], capture_output=True, text=True,
                        timeout=timeout)
-    if r.returncode != 0:
+    if "Fortran STOP" in (r.stdout + r.stderr) or "Problem" in r.stdout:
+        raise RefStop(r.stdout)
+    if r.returncode != 0 or not (Path(d) / "annual.f32").exists():
         raise RuntimeError(f"h9ref failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
     return r
 

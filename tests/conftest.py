@@ -1,0 +1,70 @@
+"""Shared test fixtures.  GPU tests are marked ``@pytest.mark.gpu``."""
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLDEN = ROOT / "tests" / "golden"
+sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long CPU test")
+
+
+def golden_names(kind=None):
+    out = []
+    for p in sorted(GOLDEN.glob("*.npz")):
+        m = json.loads(str(np.load(p)["meta"]))
+        if kind is None or m["kind"] in kind:
+            out.append(p.stem)
+    return out
+
+
+def load_golden(name):
+    """Returns (meta, inputs, expected) for a golden case.  Synthetic inputs
+    are regenerated and checked against the stored sha256."""
+    from hybrid9_amd import synth
+    from tests.golden.make_golden import digest, packed_params, synth_inputs
+    from oracle import refcase
+
+    z = np.load(GOLDEN / f"{name}.npz")
+    meta = json.loads(str(z["meta"]))
+    L = meta["L"]
+    n = meta["ncell"]
+    if meta["kind"] == "synth":
+        gid = np.asarray(meta["gid"], dtype=np.int64)
+        p, f = synth_inputs(gid, meta["year0"], meta["nyears"], L, meta["seed"])
+        assert digest(packed_params(p), f) == meta["input_sha256"], "synthetic inputs drifted"
+        state0 = None
+    else:
+        pp = z["params"]
+        p = {k: pp[i * n * L:(i + 1) * n * L].reshape(n, L)
+             for i, k in enumerate(("theta_s", "hksat", "bsw", "psi_s"))}
+        p["fmax"] = pp[4 * n * L:].copy()
+        f = z["forcing"]
+        state0 = z["state0"] if "state0" in z.files else None
+    inputs = dict(zi=np.asarray(meta["zi"], np.float32), params=p, forcing=f,
+                  nisurf=meta["nisurf"], year0=meta["year0"], nyears=meta["nyears"],
+                  grow_on=meta["grow_on"], state0=state0)
+    expected = {k: z[k] for k in ("annual", "state", "trace") if k in z.files}
+    return meta, inputs, expected
+
+
+def same_bits(a, b):
+    """Bitwise equality with NaN == NaN (any payload) and +0 == -0."""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    return a.shape == b.shape and bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+
+
+@pytest.fixture(scope="session")
+def gpu_available():
+    import hybrid9_amd as h
+    return h.lib().h9g_device_count() > 0

@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.npz from the REFERENCE itself.
+
+Runs ``oracle/_ref/h9ref`` -- the unmodified reference HYDROLOGY.f90 /
+GROW.f90 / SHARED.f90 / CONTROL.f90 compiled by ``make -C oracle ref`` --
+on synthetic inputs and stores inputs (or their checksums) and outputs.
+Needs /root/reference (build container only); the fixtures are data and
+travel with the repo.
+
+    python tests/golden/make_golden.py            # all cases
+
+Each npz holds: meta (json string), annual (nyears, 12+L, ncell),
+state (packed, refcase.state_fields), optionally trace (ntrace, nsteps, 3L+7)
+and, for cases with hand-built inputs, params / forcing / state0.
+Synthetic cases store the sha256 of their inputs instead; tests regenerate
+them with hybrid9_amd.synth and check the digest first.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+from hybrid9_amd import synth  # noqa: E402
+from oracle import refcase  # noqa: E402
+
+OUT = Path(__file__).resolve().parent
+TRACE_STEPS = 96          # keep the first two days of per-substep traces
+
+
+def digest(*arrays) -> str:
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def synth_inputs(gid, year0, nyears, L=8, seed=synth.SEED):
+    lat = synth.cell_lat(gid)
+    p = synth.make_params(gid, L, seed)
+    nd = sum(synth.days_in_year(year0 + k) for k in range(nyears))
+    f = synth.make_forcing(gid, lat, synth.year_day0(year0), nd, seed)
+    return p, f
+
+
+def packed_params(p):
+    return np.concatenate([p[k].ravel() for k in ("theta_s", "hksat", "bsw", "psi_s")]
+                          + [p["fmax"].ravel()]).astype(np.float32)
+
+
+def save(name, meta, out, extra=None):
+    d = dict(meta=np.array(json.dumps(meta)), annual=out["annual"],
+             state=refcase.pack_state(out["state"], meta["L"]))
+    if "trace" in out:
+        d["trace"] = out["trace"][:, :TRACE_STEPS, :]
+    if extra:
+        d.update(extra)
+    np.savez_compressed(OUT / f"{name}.npz", **d)
+    print(f"{name}: {meta['ncell']} cells x {meta['nyears']} yr, "
+          f"{(OUT / f'{name}.npz').stat().st_size / 1e3:.0f} kB")
+
+
+def synth_case(name, gid, *, year0=1901, nyears=1, nisurf=48, grow_on=1, trace=()):
+    gid = np.asarray(gid, dtype=np.int64)
+    p, f = synth_inputs(gid, year0, nyears)
+    out = refcase.run_case(zi=synth.ZI_L8, params=p, forcing=f, nisurf=nisurf, year0=year0,
+                           nyears=nyears, grow_on=grow_on, trace_cells=trace)
+    meta = dict(name=name, kind="synth", seed=synth.SEED, gid=gid.tolist(), L=8,
+                ncell=int(gid.size), year0=year0, nyears=nyears, nisurf=nisurf,
+                grow_on=grow_on, zi=synth.ZI_L8.tolist(), trace_cells=list(trace),
+                input_sha256=digest(packed_params(p), f),
+                generator="oracle/_ref/h9ref (reference HYDROLOGY.f90/GROW.f90, amdflang -O2)")
+    save(name, meta, out)
+
+
+def independent_layer_params(gid, L=8, seed=synth.SEED):
+    """The generator's first version: every layer drawn independently.  Such
+    columns can have extreme layer contrasts that make the reference STOP on
+    its water-balance check (kept only to build the STOP fixture)."""
+    F32 = np.float32
+    gid = np.asarray(gid, dtype=np.uint64)
+    key = gid[:, None] * np.uint64(16) + np.arange(L, dtype=np.uint64)[None, :]
+    u = lambda s, k: synth.u01(seed, s, k)  # noqa: E731
+    ks = F32(0.5) + F32(487.5) * u(synth.S_KS, key)
+    lam = np.maximum(F32(0.10) + F32(0.40) * u(synth.S_LAMBDA, key), F32(1e-8))
+    return dict(theta_s=(F32(0.30) + F32(0.30) * u(synth.S_THETA_S, key)).astype(F32),
+                hksat=((F32(10.0) * ks) / F32(86400.0)).astype(F32),
+                bsw=(F32(1.0) / lam).astype(F32),
+                psi_s=(F32(10.0) * (F32(-80.0) + F32(75.0) * u(synth.S_PSI, key))).astype(F32),
+                fmax=(F32(0.1) + F32(0.5) * u(synth.S_FMAX, gid)).astype(F32))
+
+
+def stop_case(name, gid, *, year0=1901, nisurf=24, grow_on=1):
+    """Explicit inputs on which the reference executes a STOP: the fixture
+    is the STOP site and the values the reference prints."""
+    gid = np.asarray(gid, dtype=np.int64)
+    p = independent_layer_params(gid)
+    f = synth.make_forcing(gid, synth.cell_lat(gid), synth.year_day0(year0), 365)
+    try:
+        refcase.run_case(zi=synth.ZI_L8, params=p, forcing=f, nisurf=nisurf, year0=year0,
+                         nyears=1, grow_on=grow_on)
+    except refcase.RefStop as e:
+        info = e.info
+    else:
+        raise SystemExit(f"{name}: expected a reference STOP")
+    meta = dict(name=name, kind="stop", L=8, ncell=int(gid.size), year0=year0, nyears=1,
+                nisurf=nisurf, grow_on=grow_on, zi=synth.ZI_L8.tolist(), stop=info,
+                generator="oracle/_ref/h9ref STOP output")
+    np.savez_compressed(OUT / f"{name}.npz", meta=np.array(json.dumps(meta)),
+                        params=packed_params(p), forcing=f)
+    print(f"{name}: reference STOP {info}")
+
+
+def edge_case():
+    """Hand-built states and forcing that drive every branch of HYDROLOGY
+    and GROW the synthetic climate rarely reaches (see meta['cells'])."""
+    L = 8
+    zi = synth.ZI_L8
+    dz = np.diff(zi)[:L]
+    base = synth.land_cells()[::4211][:16].astype(np.int64)
+    p, f = synth_inputs(base, 1901, 1)
+    n = base.size
+    st = refcase.unpack_state(np.zeros(n * (4 * L + 9), np.float32), n, L)
+    # INIT.f90:707-811 defaults, then per-cell overrides
+    from oracle import port
+    st = refcase.unpack_state(port.init_state(p, zi), n, L)
+    ts = p["theta_s"]
+    desc = []
+
+    def setc(c, what, **kv):
+        for k, v in kv.items():
+            st[k][c] = v
+        desc.append(f"{c}: {what}")
+
+    setc(0, "water table at surface (jwt=0), wet column", zwt=0.02,
+         h2osoi_liq=(0.95 * ts[0] * dz).astype(np.float32))
+    setc(1, "water table in layer 3 (jwt=2)", zwt=0.12)
+    setc(2, "water table in layer 8 (jwt=7)", zwt=1.5)
+    setc(3, "water table exactly at zi(8)/1000", zwt=np.float32(2296.0) / np.float32(1000.0))
+    setc(4, "saturated column", zwt=0.5, h2osoi_liq=(ts[4] * dz).astype(np.float32))
+    setc(5, "very dry and hot, no rain (theta(1)<=0.15, watmin)",
+         h2osoi_liq=(0.03 * ts[5] * dz).astype(np.float32))
+    f[5, :, 5] = 0.0
+    f[0, :, 5] += 12.0
+    setc(6, "dense canopy LAI>4", LAI=5.0, plant_foliage_mass=5.0 / 23.0e-3)
+    setc(7, "very negative smp (w_i<0.6 foliage loss)",
+         smp=np.full(L, -1.2e5, np.float32))
+    f[5, :, 8] *= 30.0
+    desc.append("8: heavy rain x30 (infiltration excess, rising water table)")
+    setc(9, "water table near the 80 m clamp", zwt=79.5)
+    setc(10, "aquifer near its 5000 mm cap", wa=4995.0, zwt=2.5)
+    f[5, :, 10] *= 10.0
+    setc(11, "no canopy, no litter, no light (rsc/rac 1e6 branches)", LAI=0.0, LAI_litter=0.0,
+         plant_foliage_mass=0.0)
+    f[2, :, 11] = 0.0
+    f[0, :, 12] = np.minimum(f[0, :, 12], 250.0) - 5.0
+    desc.append("12: cold (fT clipping)")
+    f[0, :, 13] = np.maximum(f[0, :, 13], 296.0) + 2.0
+    desc.append("13: hot, tas-tf>18 fT branch")
+    p["hksat"][14, :3] = 1.0e-5
+    f[5, :, 14] *= 15.0
+    desc.append("14: tight topsoil + heavy rain (qinmax limits infiltration)")
+    setc(15, "bottom layers near watmin", h2osoi_liq=np.array(
+        [5, 5, 5, 5, 3, 0.02, 0.011, 0.0105], np.float32) * np.float32(1.0))
+    state0 = refcase.pack_state(st, L)
+    out = refcase.run_case(zi=zi, params=p, forcing=f, nisurf=48, year0=1901, nyears=1,
+                           grow_on=1, state0=st, trace_cells=(0, 8, 15))
+    meta = dict(name="edge", kind="explicit", L=L, ncell=n, year0=1901, nyears=1, nisurf=48,
+                grow_on=1, zi=zi.tolist(), trace_cells=[0, 8, 15], cells=desc,
+                generator="oracle/_ref/h9ref (reference HYDROLOGY.f90/GROW.f90, amdflang -O2)")
+    save("edge", meta, out, extra=dict(params=packed_params(p), forcing=f, state0=state0))
+
+
+def main():
+    if not refcase.REF_BIN.exists():
+        sys.exit("build the reference harness first: make -C oracle ref")
+    g10 = np.array([(80 + j) * synth.NX05 + 400 + i for j in range(10) for i in range(10)])
+    land = synth.land_cells()
+    # config 1: 10x10 synthetic land grid, one year daily, NS=48, GROW on
+    synth_case("c1_10x10", g10, trace=(0, 37, 99))
+    # config 1 over a leap-year boundary, two years (1903-1904)
+    synth_case("c1_2yr_leap", g10[::6], year0=1903, nyears=2)
+    # config 2 sample: 0.5 deg global land cells, hydrology only
+    synth_case("c2_sample", land[::527][:128], grow_on=0, trace=(5,))
+    # config 3 sample: NS=24, GROW on
+    synth_case("c3_sample", land[263::527][:128], nisurf=24)
+    # a reference STOP (water imbalance > 0.1 mm at NS=24) on hand-built soils
+    stop_case("stop_ns24", land[263::527][90:98], nisurf=24)
+    edge_case()
+
+
+if __name__ == "__main__":
+    main()
