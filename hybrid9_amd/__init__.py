@@ -107,6 +107,7 @@ def lib() -> C.CDLL:
         "h9g_math_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP]),
         "h9g_synth_host": (C.c_int, [C.c_uint64, C.c_int, C.c_int, _I64P, _FP, C.c_int,
                                      C.c_int, _FP, _FP]),
+        "h9g_land_cells": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint64, _I64P, _FP]),
         "h9g_host_expf": (C.c_float, [C.c_float]),
         "h9g_host_powf": (C.c_float, [C.c_float, C.c_float]),
     }

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/h9g.h"
@@ -780,6 +781,32 @@ int h9g_synth_host(uint64_t seed, int nlayers, int ncell, const int64_t *gid, co
         h9s::forcing(seed, (uint64_t)gid[c], lat[c], (int64_t)day0 + d, v);
         for (int k = 0; k < 7; k++) forcing_out[(size_t)k * nday * n + (size_t)d * n + c] = v[k];
       }
+  }
+  return 0;
+}
+
+int h9g_land_cells(int nx, int ny, int nland, uint64_t seed, int64_t *gid, float *lat) {
+  if (nx <= 0 || ny <= 0 || nland <= 0 || nland > nx * ny || !gid || !lat) return H9G_EINVAL;
+  const int64_t ng = (int64_t)nx * ny;
+  std::vector<double> score(ng);
+  for (int64_t g = 0; g < ng; g++) {
+    const double iy = (double)(g / nx);
+    const double la = 90.0 - (iy + 0.5) * (180.0 / ny);
+    double c = (la + 10.0) / 70.0;
+    c = c < 0.0 ? 0.0 : (c > 1.0 ? 1.0 : c);
+    const double w = la < -60.0 ? 0.15 : (la > 80.0 ? 0.2 : 0.45 + 0.35 * c);
+    score[g] = (double)h9s::u01(seed, 1, (uint64_t)g) * w;
+  }
+  std::vector<int64_t> idx(ng);
+  for (int64_t g = 0; g < ng; g++) idx[g] = g;
+  std::nth_element(idx.begin(), idx.begin() + nland, idx.end(), [&](int64_t a, int64_t b) {
+    return score[a] > score[b] || (score[a] == score[b] && a < b);
+  });
+  std::sort(idx.begin(), idx.begin() + nland);
+  const float dlat = (float)(180.0 / ny);
+  for (int i = 0; i < nland; i++) {
+    gid[i] = idx[i];
+    lat[i] = (90.0f - dlat * 0.5f) - (float)(idx[i] / nx) * dlat;
   }
   return 0;
 }

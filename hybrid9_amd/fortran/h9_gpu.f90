@@ -1,0 +1,216 @@
+!======================================================================!
+MODULE H9_GPU
+!----------------------------------------------------------------------!
+! ISO_C_BINDING interface of libh9g.so (include/h9g.h): the Fortran side
+! of the drop-in boundary.  A HYBRID9 host replaces the cell loop of
+! /root/reference/SOURCE/HYBRID9.f90:120-295 by one h9g_run_year call per
+! simulated year (see INTEGRATION.md).  Arrays are passed by reference
+! with the SHARED.f90 layouts: per-layer (L,ncell) layer-fastest,
+! per-cell (ncell), forcing (ncell,nday) per variable stacked as
+! (ncell,nday,7) in READ_PGF.f90 order tas rlds rsds huss ps pr rhs.
+!----------------------------------------------------------------------!
+USE, INTRINSIC :: ISO_C_BINDING
+IMPLICIT NONE
+
+INTEGER, PARAMETER :: H9G_LMAX = 10
+INTEGER, PARAMETER :: H9G_NDIAG = 12
+INTEGER, PARAMETER :: H9G_ERR_TRIDIAG1 = 1, H9G_ERR_TRIDIAG2 = 2
+INTEGER, PARAMETER :: H9G_ERR_RSUB_POS = 3, H9G_ERR_IMBALANCE = 4
+
+TYPE, BIND(C) :: h9g_config
+  INTEGER(C_INT32_T) :: ncell, nlayers, nisurf, grow_on, max_days, nslots
+  REAL(C_FLOAT) :: zi (0:H9G_LMAX+1)
+END TYPE h9g_config
+
+TYPE, BIND(C) :: h9g_error
+  INTEGER(C_INT32_T) :: code, cell, year, day, substep
+  REAL(C_FLOAT) :: value
+END TYPE h9g_error
+
+INTERFACE
+  FUNCTION h9g_abi_version () BIND(C, NAME='h9g_abi_version')
+    IMPORT :: C_INT
+    INTEGER(C_INT) :: h9g_abi_version
+  END FUNCTION
+  FUNCTION h9g_device_count () BIND(C, NAME='h9g_device_count')
+    IMPORT :: C_INT
+    INTEGER(C_INT) :: h9g_device_count
+  END FUNCTION
+  FUNCTION h9g_create (cfg, device) BIND(C, NAME='h9g_create')
+    IMPORT :: C_PTR, C_INT, h9g_config
+    TYPE(h9g_config), INTENT(IN) :: cfg
+    INTEGER(C_INT), VALUE :: device
+    TYPE(C_PTR) :: h9g_create
+  END FUNCTION
+  SUBROUTINE h9g_destroy (ctx) BIND(C, NAME='h9g_destroy')
+    IMPORT :: C_PTR
+    TYPE(C_PTR), VALUE :: ctx
+  END SUBROUTINE
+  FUNCTION h9g_set_params (ctx, theta_s, hksat, bsw, psi_s, fmax) &
+           BIND(C, NAME='h9g_set_params')
+    IMPORT :: C_PTR, C_INT, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    REAL(C_FLOAT), INTENT(IN) :: theta_s (*), hksat (*), bsw (*), psi_s (*), fmax (*)
+    INTEGER(C_INT) :: h9g_set_params
+  END FUNCTION
+  FUNCTION h9g_init_state (ctx) BIND(C, NAME='h9g_init_state')
+    IMPORT :: C_PTR, C_INT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT) :: h9g_init_state
+  END FUNCTION
+  FUNCTION h9g_state_size (nlayers) BIND(C, NAME='h9g_state_size')
+    IMPORT :: C_INT
+    INTEGER(C_INT), VALUE :: nlayers
+    INTEGER(C_INT) :: h9g_state_size
+  END FUNCTION
+  FUNCTION h9g_set_state (ctx, packed) BIND(C, NAME='h9g_set_state')
+    IMPORT :: C_PTR, C_INT, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    REAL(C_FLOAT), INTENT(IN) :: packed (*)
+    INTEGER(C_INT) :: h9g_set_state
+  END FUNCTION
+  FUNCTION h9g_get_state (ctx, packed) BIND(C, NAME='h9g_get_state')
+    IMPORT :: C_PTR, C_INT, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    REAL(C_FLOAT), INTENT(OUT) :: packed (*)
+    INTEGER(C_INT) :: h9g_get_state
+  END FUNCTION
+  FUNCTION h9g_push_forcing (ctx, slot, nday, forcing, async) &
+           BIND(C, NAME='h9g_push_forcing')
+    IMPORT :: C_PTR, C_INT, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT), VALUE :: slot, nday, async
+    REAL(C_FLOAT), INTENT(IN) :: forcing (*)
+    INTEGER(C_INT) :: h9g_push_forcing
+  END FUNCTION
+  FUNCTION h9g_push_forcing_device (ctx, slot, nday, dev) &
+           BIND(C, NAME='h9g_push_forcing_device')
+    IMPORT :: C_PTR, C_INT
+    TYPE(C_PTR), VALUE :: ctx, dev
+    INTEGER(C_INT), VALUE :: slot, nday
+    INTEGER(C_INT) :: h9g_push_forcing_device
+  END FUNCTION
+  FUNCTION h9g_forcing_slot (ctx, slot) BIND(C, NAME='h9g_forcing_slot')
+    IMPORT :: C_PTR, C_INT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT), VALUE :: slot
+    TYPE(C_PTR) :: h9g_forcing_slot
+  END FUNCTION
+  FUNCTION h9g_host_alloc (bytes) BIND(C, NAME='h9g_host_alloc')
+    IMPORT :: C_PTR, C_SIZE_T
+    INTEGER(C_SIZE_T), VALUE :: bytes
+    TYPE(C_PTR) :: h9g_host_alloc
+  END FUNCTION
+  SUBROUTINE h9g_host_free (p) BIND(C, NAME='h9g_host_free')
+    IMPORT :: C_PTR
+    TYPE(C_PTR), VALUE :: p
+  END SUBROUTINE
+  FUNCTION h9g_run_year (ctx, slot, jyear) BIND(C, NAME='h9g_run_year')
+    IMPORT :: C_PTR, C_INT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT), VALUE :: slot, jyear
+    INTEGER(C_INT) :: h9g_run_year
+  END FUNCTION
+  FUNCTION h9g_sync (ctx) BIND(C, NAME='h9g_sync')
+    IMPORT :: C_PTR, C_INT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT) :: h9g_sync
+  END FUNCTION
+  FUNCTION h9g_last_error (ctx, err) BIND(C, NAME='h9g_last_error')
+    IMPORT :: C_PTR, C_INT, h9g_error
+    TYPE(C_PTR), VALUE :: ctx
+    TYPE(h9g_error), INTENT(OUT) :: err
+    INTEGER(C_INT) :: h9g_last_error
+  END FUNCTION
+  FUNCTION h9g_get_annual (ctx, annual) BIND(C, NAME='h9g_get_annual')
+    IMPORT :: C_PTR, C_INT, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    REAL(C_FLOAT), INTENT(OUT) :: annual (*)
+    INTEGER(C_INT) :: h9g_get_annual
+  END FUNCTION
+  FUNCTION h9g_get_diagnostics (ctx, host_out, dev_out) &
+           BIND(C, NAME='h9g_get_diagnostics')
+    IMPORT :: C_PTR, C_INT, C_DOUBLE
+    TYPE(C_PTR), VALUE :: ctx, dev_out
+    REAL(C_DOUBLE), INTENT(OUT) :: host_out (*)
+    INTEGER(C_INT) :: h9g_get_diagnostics
+  END FUNCTION
+  FUNCTION h9g_set_cells (ctx, gid, lat) BIND(C, NAME='h9g_set_cells')
+    IMPORT :: C_PTR, C_INT, C_INT64_T, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT64_T), INTENT(IN) :: gid (*)
+    REAL(C_FLOAT), INTENT(IN) :: lat (*)
+    INTEGER(C_INT) :: h9g_set_cells
+  END FUNCTION
+  FUNCTION h9g_synth_params (ctx, seed) BIND(C, NAME='h9g_synth_params')
+    IMPORT :: C_PTR, C_INT, C_INT64_T
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT64_T), VALUE :: seed
+    INTEGER(C_INT) :: h9g_synth_params
+  END FUNCTION
+  FUNCTION h9g_synth_forcing (ctx, slot, seed, day0, nday) &
+           BIND(C, NAME='h9g_synth_forcing')
+    IMPORT :: C_PTR, C_INT, C_INT64_T
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT), VALUE :: slot, day0, nday
+    INTEGER(C_INT64_T), VALUE :: seed
+    INTEGER(C_INT) :: h9g_synth_forcing
+  END FUNCTION
+  FUNCTION h9g_land_cells (nx, ny, nland, seed, gid, lat) &
+           BIND(C, NAME='h9g_land_cells')
+    IMPORT :: C_INT, C_INT64_T, C_FLOAT
+    INTEGER(C_INT), VALUE :: nx, ny, nland
+    INTEGER(C_INT64_T), VALUE :: seed
+    INTEGER(C_INT64_T), INTENT(OUT) :: gid (*)
+    REAL(C_FLOAT), INTENT(OUT) :: lat (*)
+    INTEGER(C_INT) :: h9g_land_cells
+  END FUNCTION
+  FUNCTION h9g_last_kernel_ms (ctx) BIND(C, NAME='h9g_last_kernel_ms')
+    IMPORT :: C_PTR, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    REAL(C_FLOAT) :: h9g_last_kernel_ms
+  END FUNCTION
+  FUNCTION h9g_total_kernel_ms (ctx, reset) BIND(C, NAME='h9g_total_kernel_ms')
+    IMPORT :: C_PTR, C_INT, C_DOUBLE
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT), VALUE :: reset
+    REAL(C_DOUBLE) :: h9g_total_kernel_ms
+  END FUNCTION
+END INTERFACE
+
+CONTAINS
+
+  !--------------------------------------------------------------------!
+  ! Print the reference's STOP diagnostics for the first failing cell
+  ! and stop, as HYDROLOGY.f90:806-825,1068-1072,1244-1274 do.
+  !--------------------------------------------------------------------!
+  SUBROUTINE h9g_check_stop (ctx, rc)
+    TYPE(C_PTR), INTENT(IN) :: ctx
+    INTEGER(C_INT), INTENT(IN) :: rc
+    TYPE(h9g_error) :: e
+    INTEGER(C_INT) :: r
+    IF (rc == 0) RETURN
+    IF (rc < 0) THEN
+      WRITE (*,*) 'h9g API/HIP failure, code ', rc
+      STOP 'h9g failure'
+    END IF
+    r = h9g_last_error (ctx, e)
+    SELECT CASE (e%code)
+    CASE (H9G_ERR_TRIDIAG1)
+      WRITE (*,*) 'Problem with tridiagonal 1.'
+    CASE (H9G_ERR_TRIDIAG2)
+      WRITE (*,*) 'Problem with tridiagonal 2.'
+    CASE (H9G_ERR_RSUB_POS)
+      WRITE (*,*) 'rsub_top_tot is positive in drainage'
+      WRITE (*,*) 'HYBRID9 is stopping'
+    CASE DEFAULT
+      WRITE (*,*) 'Problem in HYDROLOGY'
+      WRITE (*,*) 'Water imbalance > 0.1 mm ', e%value
+    END SELECT
+    WRITE (*,*) 'DiTIME = ', e%day + 1
+    WRITE (*,*) 'cell year substep ', e%cell + 1, e%year, e%substep + 1
+    STOP
+  END SUBROUTINE h9g_check_stop
+
+END MODULE H9_GPU
+!======================================================================!

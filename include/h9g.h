@@ -134,6 +134,10 @@ int h9g_get_diagnostics(h9g_ctx *ctx, double *host_out, double *dev_out);
 /* --- synthetic inputs (hybrid9_amd/synth.py, bit-identical) ----------- */
 /* Cells are identified by their grid id (iy*nx+ix) and latitude. */
 int h9g_set_cells(h9g_ctx *ctx, const int64_t *gid, const float *lat);
+/* The synthetic land mask (host): the nland grid ids of an nx x ny grid,
+ * raster order, and their latitudes (synth.land_cells / cell_lat). */
+int h9g_land_cells(int nx, int ny, int nland, uint64_t seed, int64_t *gid,
+                   float *lat);
 int h9g_synth_params(h9g_ctx *ctx, uint64_t seed);
 int h9g_synth_forcing(h9g_ctx *ctx, int slot, uint64_t seed, int day0,
                       int nday);
