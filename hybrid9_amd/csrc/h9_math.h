@@ -222,4 +222,26 @@ H9_HD float powf(float x, float y, const Tabs &T) {
   return exp2_inline(ylogx, sign_bias, T);
 }
 
+// ------------------------------------------------- normal-path variants
+// expf_nx / powf_nx run only glibc's main path (no branches) and set
+// `special` when glibc would have taken any other path for this input
+// (expf: |x| >= 88 or non-finite; powf: x not a positive normal number,
+// y zero/inf/nan, or |y log2 x| >= 126).  When `special` stays false the
+// result is bit-identical to expf/powf above; callers recompute with the
+// exact functions otherwise (h9g_step.h: speculate-then-verify substep).
+H9_HD float expf_nx(float x, const Tabs &T, bool &special) {
+  special |= ((asu32(x) >> 20) & 0x7ff) >= 0x42b;
+  return expf_core(x, T);
+}
+
+H9_HD float powf_nx(float x, float y, const Tabs &T, bool &special) {
+  const uint32_t ix = asu32(x);
+  const uint32_t iy = asu32(y);
+  const double logx = log2_inline(ix, T);
+  const double ylogx = (double)y * logx;
+  special |= (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) | zeroinfnan(iy) |
+             (((asu64(ylogx) >> 47) & 0xffff) >= (asu64(126.0) >> 47));
+  return exp2_inline(ylogx, 0, T);
+}
+
 }  // namespace h9m

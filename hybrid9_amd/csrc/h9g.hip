@@ -4,10 +4,13 @@
 // Kernel design:
 //   * h9g_year_kernel<L>: one lane = one soil column.  A launch runs one
 //     calendar year: all days x NISURF substeps of HYDROLOGY plus the daily
-//     GROW, with the whole column state, the soil parameters and the annual
-//     sums held in VGPRs.  HBM traffic per cell-day is the 7 forcing values
-//     (coalesced, cell-fastest) -- the SHARED-state contract of each
-//     substep (376 B at L=8) never leaves the register file.
+//     GROW.  The column's water state lives in VGPRs; its read-mostly data
+//     (soil parameters and their invariants, rootr, the day's constants,
+//     the substep rollback copy) in the lane's column of an LDS block, so
+//     the kernel fits 256 VGPRs (2 waves/SIMD).  HBM traffic per cell-day
+//     is the 7 forcing values (coalesced, cell-fastest) plus the annual
+//     sums (L2-resident) -- the SHARED-state contract of each substep
+//     (376 B at L=8) never leaves the CU.
 //   * glibc-exact expf/powf (h9_math.h) read their 32+16-entry tables from
 //     LDS (per-lane indices, no scalar-cache serialisation).
 //   * no MFMA: nothing here is GEMM-shaped.
@@ -25,6 +28,7 @@
 
 #include "../../include/h9g.h"
 #include "h9_math.h"
+#include "h9g_geo.h"
 #include "h9g_step.h"
 #include "h9g_synth.h"
 
@@ -36,6 +40,7 @@ static const uint64_t h_exp2tab[32] = H9M_EXP2F_TAB_INIT;
 static const double h_log2tab[32] = H9M_POWF_LOG2_TAB_INIT;
 
 #define H9G_BLOCK 256
+#define H9G_YBLOCK 64   // year kernel: one wave per block (LDS cell stores)
 #define NEVT 64
 
 // ---------------------------------------------------------------------------
@@ -64,29 +69,27 @@ __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
   __syncthreads();
 }
 
-template <int L>
-__global__ void __launch_bounds__(H9G_BLOCK) h9g_year_kernel(const KArgs a, const Geo<L> g) {
+template <int L, class G>
+__global__ void __launch_bounds__(H9G_YBLOCK) __attribute__((amdgpu_waves_per_eu(2, 2))) h9g_year_kernel(const KArgs a, const G g) {
   __shared__ uint64_t s_e2[32];
   __shared__ double s_l2[32];
+  __shared__ float s_cell[Lay<L>::N * H9G_YBLOCK];    // cell stores, [field][lane]
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= a.ncell) return;
   const int n = a.ncell;
 
-  Par<L> p;
+  CellStore<L> cs{(lds_float *)&s_cell[threadIdx.x]};
   St<L> s;
 #pragma unroll
+  for (int f = 0; f < 4 * L + 1; f++) cs.set(f, a.par[(size_t)f * n + c]);
+#pragma unroll
   for (int i = 1; i <= L; i++) {
-    p.ts[i] = a.par[(size_t)(0 * L + i - 1) * n + c];
-    p.hks[i] = a.par[(size_t)(1 * L + i - 1) * n + c];
-    p.bsw[i] = a.par[(size_t)(2 * L + i - 1) * n + c];
-    p.psi[i] = a.par[(size_t)(3 * L + i - 1) * n + c];
     s.h2o[i] = a.st[(size_t)(0 * L + i - 1) * n + c];
     s.smp[i] = a.st[(size_t)(2 * L + i - 1) * n + c];
-    s.rootr[i] = a.st[(size_t)(3 * L + i - 1) * n + c];
+    cs.set(Lay<L>::ROOTR + i - 1, a.st[(size_t)(3 * L + i - 1) * n + c]);
   }
-  p.fmax = a.par[(size_t)(4 * L) * n + c];
   const size_t o8 = (size_t)(4 * L + 1) * n + c;
   s.zwt = a.st[o8 + 0 * (size_t)n];
   s.wa = a.st[o8 + 1 * (size_t)n];
@@ -100,132 +103,73 @@ __global__ void __launch_bounds__(H9G_BLOCK) h9g_year_kernel(const KArgs a, cons
   // soil mask (HYBRID9.f90:122-123): SUM(theta_s) > trunc
   float ts_sum = zero;
 #pragma unroll
-  for (int i = 1; i <= L; i++) ts_sum = ts_sum + p.ts[i];
+  for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.get(Lay<L>::TS + i - 1);
   if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
 #pragma unroll
     for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + c] = __builtin_nanf("");
     return;
   }
-
-  float npp_sum = zero, plant_mass_sum = zero, rnf_sum = zero;
-  float tas_sum = zero, rlds_sum = zero, rsds_sum = zero, huss_sum = zero;
-  float ps_sum = zero, pr_sum = zero, rhs_sum = zero, h2osoi_sum_total = zero;
-  float theta_sum[L + 1], theta[L + 1];
-#pragma unroll
-  for (int i = 1; i <= L; i++) { theta_sum[i] = zero; theta[i] = zero; }
-  float npp = zero;
-  int code = 0, eday = 0, estep = 0;
+  cell_inv<L, G>(g, cs);
+  int eday = 0, estep = 0;
   float errval = 0.0f;
-
-  const float *f = a.forc + c;
-  for (int day = 0; day < a.nt; day++) {
-    const size_t fo = (size_t)day * n;
-    const float tas = f[fo + 0 * a.fvar];
-    const float rlds = f[fo + 1 * a.fvar];
-    const float rsds = f[fo + 2 * a.fvar];
-    const float huss = f[fo + 3 * a.fvar];
-    const float ps = f[fo + 4 * a.fvar];
-    const float pr = f[fo + 5 * a.fvar];
-    const float rhs = f[fo + 6 * a.fvar];
-    Day d;                                        // HYBRID9.f90:168-184
-    d.tak = tas;
-    d.rh = rhs;
-    d.Rnet = 0.92f * rsds + rlds - stbo * (tas * (tas * (tas * tas)));
-    d.PAR = 0.92f * rsds * 2.3f;
-    d.forc_rain = 1.0E3f * pr / rhow;
-    d.lamb = ((2503.0f - 2.386f * (d.tak - tf))) * 1.0E3f;
-    d.huss = huss;
-    d.ps = ps;
-    for (int ns = 0; ns < a.nisurf; ns++) {       // HYBRID9.f90:193-211
-      code = hydrology_step<L>(g, p, d, s, theta, rnf_sum, errval, T);
-      if (code) { eday = day; estep = ns; break; }
-    }
-    if (code) break;
-    if (a.grow_on) grow_day<L>(g, tas, s, npp, T);  // HYBRID9.f90:217
-    tas_sum = tas_sum + tas;                         // :235-254
-    rlds_sum = rlds_sum + rlds;
-    rsds_sum = rsds_sum + rsds;
-    huss_sum = huss_sum + huss;
-    ps_sum = ps_sum + ps;
-    pr_sum = pr_sum + pr;
-    rhs_sum = rhs_sum + rhs;
-    plant_mass_sum = plant_mass_sum + s.pm;
-    npp_sum = npp_sum + npp;
-#pragma unroll
-    for (int i = 1; i <= L; i++) {
-      theta_sum[i] = theta_sum[i] + theta[i];
-      h2osoi_sum_total = h2osoi_sum_total + s.h2o[i];
-    }
-  }
+  const int code = cell_year<L, G>(g, cs, s, a.forc + c, (size_t)n, a.fvar, a.nt, a.nisurf,
+                                   a.grow_on, a.annual + c, (size_t)n, eday, estep, errval, T);
+  int cw = c;            // recompute write-back addresses rather than keep the load ones live
+  opaque(cw);
+  cs.launder();
 
   // state write-back
+  const size_t ow = (size_t)(4 * L + 1) * n + cw;
 #pragma unroll
   for (int i = 1; i <= L; i++) {
-    a.st[(size_t)(0 * L + i - 1) * n + c] = s.h2o[i];
-    a.st[(size_t)(2 * L + i - 1) * n + c] = s.smp[i];
-    if (a.grow_on) a.st[(size_t)(3 * L + i - 1) * n + c] = s.rootr[i];
+    a.st[(size_t)(0 * L + i - 1) * n + cw] = s.h2o[i];
+    a.st[(size_t)(2 * L + i - 1) * n + cw] = s.smp[i];
+    if (a.grow_on) a.st[(size_t)(3 * L + i - 1) * n + cw] = cs.get(Lay<L>::ROOTR + i - 1);
   }
-  if (a.grow_on) a.st[(size_t)(4 * L) * n + c] = zero;   // rootr_col(Nlevgrnd)
-  a.st[o8 + 0 * (size_t)n] = s.zwt;
-  a.st[o8 + 1 * (size_t)n] = s.wa;
-  a.st[o8 + 2 * (size_t)n] = s.LAI;
-  a.st[o8 + 3 * (size_t)n] = s.LAI_litter;
-  a.st[o8 + 4 * (size_t)n] = s.pm;
-  a.st[o8 + 5 * (size_t)n] = s.pfm;
-  a.st[o8 + 6 * (size_t)n] = s.plen;
-  a.st[o8 + 7 * (size_t)n] = s.rdepth;
+  if (a.grow_on) a.st[(size_t)(4 * L) * n + cw] = zero;   // rootr_col(Nlevgrnd)
+  a.st[ow + 0 * (size_t)n] = s.zwt;
+  a.st[ow + 1 * (size_t)n] = s.wa;
+  a.st[ow + 2 * (size_t)n] = s.LAI;
+  a.st[ow + 3 * (size_t)n] = s.LAI_litter;
+  a.st[ow + 4 * (size_t)n] = s.pm;
+  a.st[ow + 5 * (size_t)n] = s.pfm;
+  a.st[ow + 6 * (size_t)n] = s.plen;
+  a.st[ow + 7 * (size_t)n] = s.rdepth;
 
   if (code) {
-    a.err[0 * (size_t)n + c] = code;
-    a.err[1 * (size_t)n + c] = eday;
-    a.err[2 * (size_t)n + c] = estep;
-    a.err[3 * (size_t)n + c] = __builtin_bit_cast(int, errval);
+    a.err[0 * (size_t)n + cw] = code;
+    a.err[1 * (size_t)n + cw] = eday;
+    a.err[2 * (size_t)n + cw] = estep;
+    a.err[3 * (size_t)n + cw] = __builtin_bit_cast(int, errval);
     atomicOr(a.err_flag, 1);
 #pragma unroll
-    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + c] = __builtin_nanf("");
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + cw] = __builtin_nanf("");
     return;
   }
-  // annual means (HYBRID9.f90:263-290)
-  const int nt = a.nt;
-  float *an = a.annual + c;
-  an[0 * (size_t)n] = npp_sum;
-  an[1 * (size_t)n] = plant_mass_sum / (float)nt;
-  an[2 * (size_t)n] = rnf_sum / (float)(nt * a.nisurf);
-  an[3 * (size_t)n] = zero / (float)(nt * a.nisurf);   // evap_sum is never accumulated
-  an[4 * (size_t)n] = tas_sum / (float)nt;
-  an[5 * (size_t)n] = rlds_sum / (float)nt;
-  an[6 * (size_t)n] = rsds_sum / (float)nt;
-  an[7 * (size_t)n] = huss_sum / (float)nt;
-  an[8 * (size_t)n] = ps_sum / (float)nt;
-  an[9 * (size_t)n] = pr_sum / (float)nt;
-  an[10 * (size_t)n] = rhs_sum / (float)nt;
-#pragma unroll
-  for (int i = 1; i <= L; i++) an[(size_t)(10 + i) * n] = theta_sum[i] / (float)nt;
-  an[(size_t)(11 + L) * n] = h2osoi_sum_total / (float)nt;
 }
 
-template <int L>
+template <int L, class G>
 __global__ void __launch_bounds__(H9G_BLOCK) h9g_init_kernel(int ncell, const float *__restrict__ par,
-                                                             float *__restrict__ st, const Geo<L> g) {
+                                                             float *__restrict__ st, const G g) {
   __shared__ uint64_t s_e2[32];
   __shared__ double s_l2[32];
   load_tabs(s_e2, s_l2);
-  const h9m::Tabs T = {s_e2, s_l2};
+  MathExact me{{s_e2, s_l2}};
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ncell) return;
   const int n = ncell;
-  Par<L> p;
+  float ts[L + 1];
   St<L> s;
-  float h2o_ma[L + 1];
+  float h2o_ma[L + 1], rootr[L + 1];
 #pragma unroll
-  for (int i = 1; i <= L; i++) p.ts[i] = par[(size_t)(i - 1) * n + c];
-  init_cell<L>(g, p, s, h2o_ma, T);
+  for (int i = 1; i <= L; i++) ts[i] = par[(size_t)(i - 1) * n + c];
+  init_cell<L, G, MathExact>(g, ts, s, rootr, h2o_ma, me);
 #pragma unroll
   for (int i = 1; i <= L; i++) {
     st[(size_t)(0 * L + i - 1) * n + c] = s.h2o[i];
     st[(size_t)(1 * L + i - 1) * n + c] = h2o_ma[i];
     st[(size_t)(2 * L + i - 1) * n + c] = s.smp[i];
-    st[(size_t)(3 * L + i - 1) * n + c] = s.rootr[i];
+    st[(size_t)(3 * L + i - 1) * n + c] = rootr[i];
   }
   st[(size_t)(4 * L) * n + c] = zero;
   const size_t o8 = (size_t)(4 * L + 1) * n + c;
@@ -361,17 +305,41 @@ static int days_in_year(int y) {   // INIT.f90:844-859
   return 366;
 }
 
-template <int L>
-static Geo<L> make_geo(const h9g_config &c) {
-  Geo<L> g;
-  for (int i = 0; i <= L + 1; i++) g.zi[i] = c.zi[i];
-  for (int i = 1; i <= L; i++) g.dz[i] = g.zi[i] - g.zi[i - 1];
-  for (int i = 1; i <= L; i++) g.zc[i] = g.zi[i] - g.dz[i] / 2.0f;
-  for (int i = 1; i <= L; i++) g.zi_m[i] = g.zi[i] / 1000.0f;
-  g.dz[0] = g.zc[0] = g.zi_m[0] = 0.0f;
-  g.dt = 86400.0f / (float)c.nisurf;              // INIT.f90:214
-  return g;
+// Kernel variant for a context: compile-time geometry when zi is one of
+// the built-in layer sets and NISURF is 24 or 48, runtime geometry otherwise.
+enum GeoKind { GEO_R = 0, GEO_C24 = 24, GEO_C48 = 48 };
+
+static GeoKind geo_kind(const h9g_config &c) {
+  const float *zd = c.nlayers == 8 ? ZiDefault<8>::zi : ZiDefault<10>::zi;
+  for (int i = 0; i <= c.nlayers + 1; i++)
+    if (c.zi[i] != zd[i]) return GEO_R;
+  if (c.nisurf == 24) return GEO_C24;
+  if (c.nisurf == 48) return GEO_C48;
+  return GEO_R;
 }
+
+// Launch a templated kernel K<L, G> with the context's geometry variant.
+#define H9G_DISPATCH(ctx, KERNEL, GRID, BLOCK, STREAM, ...)                          \
+  do {                                                                               \
+    const GeoKind gk_ = geo_kind((ctx)->cfg);                                        \
+    if ((ctx)->L == 8) {                                                             \
+      if (gk_ == GEO_C48)                                                            \
+        KERNEL<8, GeoC<8, 48>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__, GeoC<8, 48>()); \
+      else if (gk_ == GEO_C24)                                                       \
+        KERNEL<8, GeoC<8, 24>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__, GeoC<8, 24>()); \
+      else                                                                           \
+        KERNEL<8, GeoR<8>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__,                  \
+                                                       make_geo_r<8>((ctx)->cfg.zi, (ctx)->cfg.nisurf)); \
+    } else {                                                                         \
+      if (gk_ == GEO_C48)                                                            \
+        KERNEL<10, GeoC<10, 48>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__, GeoC<10, 48>()); \
+      else if (gk_ == GEO_C24)                                                       \
+        KERNEL<10, GeoC<10, 24>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__, GeoC<10, 24>()); \
+      else                                                                           \
+        KERNEL<10, GeoR<10>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__,                \
+                                                         make_geo_r<10>((ctx)->cfg.zi, (ctx)->cfg.nisurf)); \
+    }                                                                                \
+  } while (0)
 
 static unsigned nblocks(size_t n) { return (unsigned)((n + H9G_BLOCK - 1) / H9G_BLOCK); }
 
@@ -456,7 +424,12 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     h9g_destroy(ctx);
     return nullptr;
   }
-  ctx->kname = (L == 8) ? "h9g_year_kernel<8>" : "h9g_year_kernel<10>";
+  static const char *names[2][3] = {{"h9g_year_kernel<8,GeoR>", "h9g_year_kernel<8,GeoC<8,24>>",
+                                     "h9g_year_kernel<8,GeoC<8,48>>"},
+                                    {"h9g_year_kernel<10,GeoR>", "h9g_year_kernel<10,GeoC<10,24>>",
+                                     "h9g_year_kernel<10,GeoC<10,48>>"}};
+  const GeoKind gk = geo_kind(*cfg);
+  ctx->kname = names[L == 8 ? 0 : 1][gk == GEO_R ? 0 : (gk == GEO_C24 ? 1 : 2)];
   return ctx;
 }
 
@@ -484,10 +457,7 @@ int h9g_init_state(h9g_ctx *ctx) {
   if (!ctx->params_set) return H9G_ESTATE;
   HIPCHK(hipSetDevice(ctx->device));
   const int n = (int)ctx->n;
-  if (ctx->L == 8)
-    h9g_init_kernel<8><<<nblocks(n), H9G_BLOCK, 0, ctx->sc>>>(n, ctx->d_par, ctx->d_st, make_geo<8>(ctx->cfg));
-  else
-    h9g_init_kernel<10><<<nblocks(n), H9G_BLOCK, 0, ctx->sc>>>(n, ctx->d_par, ctx->d_st, make_geo<10>(ctx->cfg));
+  H9G_DISPATCH(ctx, h9g_init_kernel, nblocks(n), H9G_BLOCK, ctx->sc, n, ctx->d_par, ctx->d_st);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemsetAsync(ctx->d_err, 0, sizeof(int) * 4 * ctx->n, ctx->sc));
   HIPCHK(hipMemsetAsync(ctx->d_errflag, 0, sizeof(int), ctx->sc));
@@ -615,10 +585,8 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   }
   const int e = ctx->nev++;
   HIPCHK(hipEventRecord(ctx->ev0[e], ctx->sc));
-  if (ctx->L == 8)
-    h9g_year_kernel<8><<<nblocks(ctx->n), H9G_BLOCK, 0, ctx->sc>>>(a, make_geo<8>(ctx->cfg));
-  else
-    h9g_year_kernel<10><<<nblocks(ctx->n), H9G_BLOCK, 0, ctx->sc>>>(a, make_geo<10>(ctx->cfg));
+  H9G_DISPATCH(ctx, h9g_year_kernel, (unsigned)((ctx->n + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
+               ctx->sc, a);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1[e], ctx->sc));
   HIPCHK(hipEventRecord(ctx->ev_consumed[slot], ctx->sc));

@@ -1,0 +1,88 @@
+"""The GPU kernel body (hybrid9_amd/csrc/h9g_step.h) compiled for the host
+(tests/csrc/host_kernel.cpp, test-only) against the reference goldens and
+the oracle, bit-for-bit -- both geometry policies (compile-time default
+layers and runtime layers).  Lets the kernel's arithmetic be checked on
+CPU; the GPU tests then check the device build."""
+import ctypes as C
+import subprocess
+
+import numpy as np
+import pytest
+
+from hybrid9_amd import synth
+from oracle import port, refcase
+from tests.conftest import golden_names, load_golden, same_bits
+from tests.helpers import BUILD, ROOT
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = ROOT / "tests" / "csrc" / "host_kernel.cpp"
+        out = BUILD / "libhost_kernel.so"
+        deps = [src] + list((ROOT / "hybrid9_amd" / "csrc").glob("*.h"))
+        if not out.exists() or out.stat().st_mtime < max(d.stat().st_mtime for d in deps):
+            BUILD.mkdir(exist_ok=True)
+            subprocess.run(["g++", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fopenmp",
+                            "-std=c++17", "-fPIC", "-shared", str(src), "-o", str(out)], check=True)
+        _lib = C.CDLL(str(out))
+        fp = C.POINTER(C.c_float)
+        _lib.h9k_host_run.argtypes = [C.c_int] * 7 + [fp, fp, fp, fp, fp, C.POINTER(C.c_int)]
+    return _lib
+
+
+def host_run(*, zi, params, forcing, nisurf, year0, nyears, grow_on, state0, const_geo):
+    L = params["theta_s"].shape[1]
+    n = params["fmax"].size
+    zi = np.ascontiguousarray(zi, np.float32)
+    pp = port.pack_params(params)
+    fo = np.ascontiguousarray(forcing, np.float32)
+    st = port.init_state(params, zi) if state0 is None else np.array(state0, np.float32)
+    ann = np.zeros((nyears, 12 + L, n), np.float32)
+    err = np.zeros(4 * n, np.int32)
+    fp = C.POINTER(C.c_float)
+    rc = lib().h9k_host_run(n, L, nisurf, int(grow_on), year0, nyears, int(const_geo),
+                            zi.ctypes.data_as(fp), pp.ctypes.data_as(fp), fo.ctypes.data_as(fp),
+                            st.ctypes.data_as(fp), ann.ctypes.data_as(fp),
+                            err.ctypes.data_as(C.POINTER(C.c_int)))
+    return dict(rc=rc, annual=ann, state=st, err=err.reshape(n, 4))
+
+
+@pytest.mark.parametrize("const_geo", [1, 0])
+@pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit")))
+def test_kernel_body_matches_reference_golden(name, const_geo):
+    meta, inp, exp = load_golden(name)
+    out = host_run(const_geo=const_geo, **inp)
+    assert out["rc"] == 0
+    assert same_bits(out["annual"], exp["annual"])
+    assert same_bits(out["state"], exp["state"])
+
+
+def test_kernel_body_reproduces_reference_stop():
+    meta, inp, _ = load_golden("stop_ns24")
+    out = host_run(const_geo=1, **inp)
+    s = meta["stop"]
+    assert out["rc"] == s["code"]
+    c = s["cell"]
+    assert out["err"][c, 0] == s["code"] and out["err"][c, 2] == s["day"]
+
+
+@pytest.mark.parametrize("L,nisurf,grow", [(8, 48, 0), (8, 24, 1), (10, 24, 1), (10, 48, 0)])
+def test_kernel_body_matches_oracle_random_cells(L, nisurf, grow):
+    if L == 8:
+        g = synth.land_cells()[7::389][:160]
+        lat, zi = synth.cell_lat(g), synth.ZI_L8
+    else:
+        g = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)[11::1601][:160]
+        lat, zi = synth.cell_lat(g, synth.NX025, synth.NY025), synth.ZI_L10
+    p = synth.make_params(g, L)
+    f = synth.make_forcing(g, lat, synth.year_day0(1903), 365 + 366)
+    ref = port.run(zi=zi, params=p, forcing=f, nisurf=nisurf, year0=1903, nyears=2,
+                   grow_on=grow, nthreads=8)
+    out = host_run(zi=zi, params=p, forcing=f, nisurf=nisurf, year0=1903, nyears=2,
+                   grow_on=grow, state0=None, const_geo=1)
+    assert ref["rc"] == out["rc"] == 0
+    assert same_bits(out["annual"], ref["annual"])
+    assert same_bits(out["state"], refcase.pack_state(ref["state"], L))

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Summarise a tools/prof.sh output dir into profiles/pmc_<tag>.json and copy
+the rocprofv3 --stats kernel table to profiles/<tag>_kernel_stats.csv.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come
+from separate --pmc passes, in KiB; on gfx950 FETCH_SIZE reports half the
+bytes of a coalesced streaming read, so it is doubled."""
+import csv
+import json
+import shutil
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def counters(d: Path, kernel: str):
+    out = defaultdict(list)
+    for f in d.glob("*/*_counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Kernel_Name"]:
+                out[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in out.items()}, {k: len(v) for k, v in out.items()}
+
+
+def main(tag, workload="config2", kernel="h9g_year_kernel"):
+    d = ROOT / "gpurun_out" / f"prof_{tag}"
+    c, n = counters(d, kernel)
+    stats = list(csv.DictReader(open(d / "kt" / "kt_kernel_stats.csv")))
+    ks = [r for r in stats if kernel in r["Name"]][0]
+    avg_ns = float(ks["AverageNs"])
+    fetch = 2.0 * c["FETCH_SIZE"] * 1024 if "FETCH_SIZE" in c else None
+    write = c["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in c else None
+    waves = c.get("SQ_WAVES")
+    res = {
+        "tag": tag, "workload": workload, "kernel": ks["Name"],
+        "source": f"rocprofv3 --pmc (separate FETCH_SIZE / WRITE_SIZE passes), profiles/pmc_{tag}.json",
+        "kernel_avg_ns_rocprof": avg_ns, "launches": int(ks["Calls"]),
+        "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+        "hbm_bytes_per_launch": (fetch or 0) + (write or 0) if fetch is not None else None,
+        "hbm_GBps_measured": ((fetch or 0) + (write or 0)) / (avg_ns * 1e-9) / 1e9 if fetch else None,
+        "counters_per_launch": c,
+    }
+    if waves:
+        res["per_wave"] = {k: v / waves for k, v in c.items() if k.startswith("SQ_INSTS")}
+    (ROOT / "profiles" / f"pmc_{tag}.json").write_text(json.dumps(res, indent=1))
+    shutil.copy(d / "kt" / "kt_kernel_stats.csv", ROOT / "profiles" / f"{tag}_kernel_stats.csv")
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
