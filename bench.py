@@ -96,7 +96,7 @@ def cpu_baseline(workload: dict, seed: int) -> dict:
 
     P = int(os.environ.get("H9_CPU_PROCS", os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
     P = max(1, min(P, os.cpu_count() or 1, 64))
-    C = int(os.environ.get("H9_CPU_CELLS", "512"))
+    C = int(os.environ.get("H9_CPU_CELLS", "2048"))
     L, ns, grow = workload["nlayers"], workload["nisurf"], int(workload["grow_on"])
     kind = "reference" if refcase.REF_BIN.exists() and L == 8 else "port"
     land = synth.land_cells()
