@@ -252,6 +252,15 @@ __global__ void __launch_bounds__(H9G_BLOCK) h9g_synth_forcing_kernel(int ncell,
   for (int k = 0; k < 7; k++) forc[k * fvar + (size_t)d * ncell + c] = v[k];
 }
 
+// MathFast's division path with a device-computed reciprocal (recip64).
+__global__ void h9g_div_kernel(int n, const float *x, const float *d, float *out, int *flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  MathFast mf{{nullptr, nullptr}, false};
+  out[i] = mf.div(x[i], d[i], recip64(d[i]));
+  flag[i] = mf.special ? 1 : 0;
+}
+
 __global__ void h9g_math_kernel(int n, const float *x, const float *y, float *out) {
   __shared__ uint64_t s_e2[32];
   __shared__ double s_l2[32];
@@ -720,6 +729,28 @@ int h9g_math_selftest(int device, int n, const float *x, const float *y, float *
   (void)hipFree(dx);
   (void)hipFree(dy);
   (void)hipFree(dout);
+  return 0;
+}
+
+int h9g_div_selftest(int device, int n, const float *x, const float *d, float *out, int *flag) {
+  if (n <= 0 || !x || !d || !out || !flag) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(device));
+  float *dx = nullptr, *dd = nullptr, *dout = nullptr;
+  int *dflag = nullptr;
+  HIPCHK(hipMalloc(&dx, sizeof(float) * n));
+  HIPCHK(hipMalloc(&dd, sizeof(float) * n));
+  HIPCHK(hipMalloc(&dout, sizeof(float) * n));
+  HIPCHK(hipMalloc(&dflag, sizeof(int) * n));
+  HIPCHK(hipMemcpy(dx, x, sizeof(float) * n, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dd, d, sizeof(float) * n, hipMemcpyHostToDevice));
+  h9g_div_kernel<<<(n + 255) / 256, 256>>>(n, dx, dd, dout, dflag);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, sizeof(float) * n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(flag, dflag, sizeof(int) * n, hipMemcpyDeviceToHost));
+  (void)hipFree(dx);
+  (void)hipFree(dd);
+  (void)hipFree(dout);
+  (void)hipFree(dflag);
   return 0;
 }
 

@@ -83,16 +83,55 @@ H9K_HD bool any_lane(bool p) {
 }
 
 // ------------------------------------------------------------ math policies
+H9K_HD bool is_subnormal(float q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_classf(q, 0x090);     // -denormal | +denormal
+#else
+  const uint32_t u = __builtin_bit_cast(uint32_t, q) & 0x7fffffffu;
+  return u != 0 && u < 0x00800000u;
+#endif
+}
+
+// Reciprocal of a float divisor in double, |r - 1/d| <= 1.2 * 2^-53 |1/d|:
+// hardware estimate + two Newton steps (each squares the error and adds
+// <= 2^-53; two steps suffice from any estimate within 2^-14).
+H9K_HD double recip64(float d) {
+  const double dd = (double)d;
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r = __builtin_amdgcn_rcp(dd);
+#else
+  double r = 1.0 / dd;
+#endif
+  double e = __builtin_fma(-dd, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-dd, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  return r;
+}
+
+// Division policy.  MathExact divides; MathFast computes RN32(RN64(x * r))
+// from a double reciprocal r of the divisor d with relative error
+// <= 2^-52.  That equals the correctly rounded x/d whenever the result is
+// a normal float: a float quotient that is not itself a rounding midpoint
+// lies at least 2^-49 (relative) away from every midpoint (x and d have
+// 24-bit significands), and a normal-range quotient is never exactly a
+// midpoint.  Subnormal results flag the substep for the exact re-run.
 struct MathExact {
   h9m::Tabs T;
   H9K_HD float expf(float x) { return h9m::expf(x, T); }
   H9K_HD float powf(float x, float y) { return h9m::powf(x, y, T); }
+  H9K_HD float div(float x, float d, double) { return x / d; }
 };
 struct MathFast {
   h9m::Tabs T;
   bool special;
   H9K_HD float expf(float x) { return h9m::expf_nx(x, T, special); }
   H9K_HD float powf(float x, float y) { return h9m::powf_nx(x, y, T, special); }
+  H9K_HD float div(float x, float, double r) {
+    const float q = (float)((double)x * r);
+    special |= is_subnormal(q);
+    return q;
+  }
 };
 
 // ------------------------------------------------------------ cell data
@@ -267,6 +306,7 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
                           float &errval, M &m) {
   typedef Lay<L> Y;
   const float dt = g.dt();
+  constexpr double r1000 = 1.0 / 1000.0;
   float zim[L + 1];
 #pragma unroll
   for (int i = 1; i <= L; i++) zim[i] = g.zim(i);
@@ -286,7 +326,7 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
 #pragma unroll
   for (int i = 1; i <= L; i++) {
     w0 = w0 + h2o[i];
-    theta[i] = h2o[i] / g.thk(i);
+    theta[i] = m.div(h2o[i], g.thk(i), g.rthk(i));
   }
   // :161-212
   const float qflx_top_soil = DC(D_FORC);
@@ -299,7 +339,7 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
   float beta = zero;
 #pragma unroll
   for (int i = 1; i <= L; i++) {
-    float b = one - (smp[i] - g.zc(i)) / (-150000.0f);
+    float b = one - m.div(smp[i] - g.zc(i), -150000.0f, 1.0 / -150000.0);
     b = MINF(one, b);
     b = MAXF(zero, b);
     beta = beta + ROOT(i) * b;
@@ -333,7 +373,7 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
   const float tran = LEc * 1.0E3f / DC(D_RL);
   float evg = LEs * 1.0E3f / DC(D_RL);
   // :396-400
-  float em1 = g.dz(1) * (theta[1] - watmin) / dt - tran * ROOT(1);
+  float em1 = m.div(g.dz(1) * (theta[1] - watmin), dt, g.rdt()) - tran * ROOT(1);
   em1 = MAXF(zero, em1);
   evg = MINF(em1, evg);
   // :426-478
@@ -361,8 +401,8 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
       if ((zwtmm < g.zi(i)) && (zwtmm > g.zi(i - 1))) {
         const float tempi = one;
         const float voleq1 = INV(PTE, i) / (zwtmm - g.zi(i - 1)) * (tempi - temp0);
-        vol_eq = (voleq1 * (zwtmm - g.zi(i - 1)) + TS(i) * (g.zi(i) - zwtmm)) /
-                 (g.zi(i) - g.zi(i - 1));
+        vol_eq = m.div(voleq1 * (zwtmm - g.zi(i - 1)) + TS(i) * (g.zi(i) - zwtmm), g.dz(i),
+                       g.rdz(i));
         vol_eq = MINF(TS(i), vol_eq);
         vol_eq = MAXF(vol_eq, zero);
       } else {
@@ -413,53 +453,57 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
   // tridiagonal system, rows 1..L+1 (:661-799)
   float amx[L + 2], bmx[L + 2], cmx[L + 2], rmx[L + 2];
   {
-    const float den = (g.zc(2) - g.zc(1));
+    const float den = g.den(1);                     // zc(2)-zc(1)
+    const double rden = g.rden(1);
     const float dzq = (zq[2] - zq[1]);
     const float num = (smp[2] - smp[1]) - dzq;
-    const float qout = -hk[1] * num / den;
-    const float dqodw1 = -(-hk[1] * dsmpdw[1] + num * dhkdw[1]) / den;
-    const float dqodw2 = -(hk[1] * dsmpdw[2] + num * dhkdw[1]) / den;
+    const float qout = m.div(-hk[1] * num, den, rden);
+    const float dqodw1 = m.div(-(-hk[1] * dsmpdw[1] + num * dhkdw[1]), den, rden);
+    const float dqodw2 = m.div(-(hk[1] * dsmpdw[2] + num * dhkdw[1]), den, rden);
     rmx[1] = qflx_infl - qout - tran * ROOT(1);
     amx[1] = zero;
-    bmx[1] = g.dz(1) / dt + dqodw1;
+    bmx[1] = m.div(g.dz(1), dt, g.rdt()) + dqodw1;
     cmx[1] = dqodw2;
   }
 #pragma unroll
   for (int i = 2; i <= L - 1; i++) {
-    float den = g.zc(i) - g.zc(i - 1);
+    float den = g.den(i - 1);                       // zc(I)-zc(I-1)
+    double rden = g.rden(i - 1);
     float dzq = zq[i] - zq[i - 1];
     float num = smp[i] - smp[i - 1] - dzq;
-    const float qin = -hk[i - 1] * num / den;
-    const float dqidw0 = -(-hk[i - 1] * dsmpdw[i - 1] + num * dhkdw[i - 1]) / den;
-    const float dqidw1 = -(hk[i - 1] * dsmpdw[i] + num * dhkdw[i - 1]) / den;
-    den = g.zc(i + 1) - g.zc(i);
+    const float qin = m.div(-hk[i - 1] * num, den, rden);
+    const float dqidw0 = m.div(-(-hk[i - 1] * dsmpdw[i - 1] + num * dhkdw[i - 1]), den, rden);
+    const float dqidw1 = m.div(-(hk[i - 1] * dsmpdw[i] + num * dhkdw[i - 1]), den, rden);
+    den = g.den(i);                                 // zc(I+1)-zc(I)
+    rden = g.rden(i);
     dzq = zq[i + 1] - zq[i];
     num = (smp[i + 1] - smp[i]) - dzq;
-    const float qout = -hk[i] * num / den;
-    const float dqodw1 = -(-hk[i] * dsmpdw[i] + num * dhkdw[i]) / den;
-    const float dqodw2 = -(hk[i] * dsmpdw[i + 1] + num * dhkdw[i]) / den;
+    const float qout = m.div(-hk[i] * num, den, rden);
+    const float dqodw1 = m.div(-(-hk[i] * dsmpdw[i] + num * dhkdw[i]), den, rden);
+    const float dqodw2 = m.div(-(hk[i] * dsmpdw[i + 1] + num * dhkdw[i]), den, rden);
     rmx[i] = qin - qout - tran * ROOT(i);
     amx[i] = -dqidw0;
-    bmx[i] = g.dz(i) / dt - dqidw1 + dqodw1;
+    bmx[i] = m.div(g.dz(i), dt, g.rdt()) - dqidw1 + dqodw1;
     cmx[i] = dqodw2;
   }
   {
     constexpr int i = L;
-    float den = g.zc(i) - g.zc(i - 1);
+    float den = g.den(i - 1);
+    const double rden0 = g.rden(i - 1);
     float dzq = zq[i] - zq[i - 1];
     float num = smp[i] - smp[i - 1] - dzq;
-    const float qin = -hk[i - 1] * num / den;
-    const float dqidw0 = -(-hk[i - 1] * dsmpdw[i - 1] + num * dhkdw[i - 1]) / den;
-    const float dqidw1 = -(hk[i - 1] * dsmpdw[i] + num * dhkdw[i - 1]) / den;
+    const float qin = m.div(-hk[i - 1] * num, den, rden0);
+    const float dqidw0 = m.div(-(-hk[i - 1] * dsmpdw[i - 1] + num * dhkdw[i - 1]), den, rden0);
+    const float dqidw1 = m.div(-(hk[i - 1] * dsmpdw[i] + num * dhkdw[i - 1]), den, rden0);
     amx[i] = -dqidw0;
     if (i > jwt) {                 // water table inside the column
       const float qout = zero, dqodw1 = zero;
       rmx[i] = qin - qout - tran * ROOT(i);
-      bmx[i] = g.dz(i) / dt - dqidw1 + dqodw1;
+      bmx[i] = m.div(g.dz(i), dt, g.rdt()) - dqidw1 + dqodw1;
       cmx[i] = zero;
       rmx[i + 1] = zero;
       amx[i + 1] = zero;
-      bmx[i + 1] = dzA / dt;
+      bmx[i + 1] = m.div(dzA, dt, g.rdt());
       cmx[i + 1] = zero;
     } else {                       // below: aquifer row
       float s_node = MAXF(0.5f * (one + theta[i] / TS(i)), 0.01f);
@@ -468,36 +512,40 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
       smp1 = MAXF(smpmin, smp1);
       const float dsmpdw1 = -BSW(i) * smp1 / (s_node * TS(i));
       den = zcA - g.zc(i);
+      const double rden = recip64(den);
       dzq = zq[i + 1] - zq[i];
       num = smp1 - smp[i] - dzq;
-      const float qout = -hk[i] * num / den;
-      const float dqodw1 = -(-hk[i] * dsmpdw[i] + num * dhkdw[i]) / den;
-      const float dqodw2 = -(hk[i] * dsmpdw1 + num * dhkdw[i]) / den;
+      const float qout = m.div(-hk[i] * num, den, rden);
+      const float dqodw1 = m.div(-(-hk[i] * dsmpdw[i] + num * dhkdw[i]), den, rden);
+      const float dqodw2 = m.div(-(hk[i] * dsmpdw1 + num * dhkdw[i]), den, rden);
       rmx[i] = qin - qout - tran * ROOT(i);
-      bmx[i] = g.dz(i) / dt - dqidw1 + dqodw1;
+      bmx[i] = m.div(g.dz(i), dt, g.rdt()) - dqidw1 + dqodw1;
       cmx[i] = dqodw2;
       const float qin1 = qout;
-      const float dqidw0b = -(-hk[i] * dsmpdw[i] + num * dhkdw[i]) / den;
-      const float dqidw1b = -(hk[i] * dsmpdw1 + num * dhkdw[i]) / den;
+      const float dqidw0b = dqodw1;    // the same expression (:787-788 vs :769-770)
+      const float dqidw1b = dqodw2;    // (:789-790 vs :771-772)
       const float qout1 = zero, dqodw1b = zero;
       rmx[i + 1] = qin1 - qout1;
       amx[i + 1] = -dqidw0b;
-      bmx[i + 1] = dzA / dt - dqidw1b + dqodw1b;
+      bmx[i + 1] = m.div(dzA, dt, g.rdt()) - dqidw1b + dqodw1b;
       cmx[i + 1] = zero;
     }
   }
   // :806-837 Thomas algorithm
   if (bmx[1] == 0.0f) { errval = bmx[1]; return 1; }
   float dwat2[L + 2], GAM[L + 2];
+  // each pivot's reciprocal serves both quotients of its row (MathFast)
   float BET = bmx[1];
-  dwat2[1] = rmx[1] / BET;
+  double rbet = recip64(BET);
+  dwat2[1] = m.div(rmx[1], BET, rbet);
   int zero_pivot = 0;
 #pragma unroll
   for (int i = 2; i <= L + 1; i++) {
-    GAM[i] = cmx[i - 1] / BET;
+    GAM[i] = m.div(cmx[i - 1], BET, rbet);
     BET = bmx[i] - amx[i] * GAM[i];
     if (BET == 0.0f && !zero_pivot) zero_pivot = i;
-    dwat2[i] = (rmx[i] - amx[i] * dwat2[i - 1]) / BET;
+    rbet = recip64(BET);
+    dwat2[i] = m.div(rmx[i] - amx[i] * dwat2[i - 1], BET, rbet);
   }
   if (zero_pivot) { errval = (float)zero_pivot; return 2; }
 #pragma unroll
@@ -529,7 +577,7 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
     qcharge = MAXF(-10.0f / dt, qcharge);
     qcharge = MINF(10.0f / dt, qcharge);
   } else {
-    qcharge = dwat2[L + 1] * dzA / dt;
+    qcharge = m.div(dwat2[L + 1] * dzA, dt, g.rdt());
   }
   // :923-1009 water table from recharge.  The jwt recomputed at :923-931
   // equals the one above (zwt unchanged since :499).  Specific yields
@@ -549,7 +597,7 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
   int jwt2 = jwt;
   if (jwt == L) {
     s.wa = s.wa + qcharge * dt;
-    s.zwt = s.zwt - (qcharge * dt) / 1000.0f / rous;
+    s.zwt = s.zwt - m.div(qcharge * dt, 1000.0f, r1000) / rous;
   } else {
     float qcharge_tot = qcharge * dt;
     if (qcharge_tot > zero) {          // rising: I = jwt+1 .. 1
@@ -560,7 +608,7 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
           const float s_y = sy[i];
           float qcl = MINF(qcharge_tot, s_y * (zwtmm - g.zi(i - 1)));
           qcl = MAXF(qcl, zero);
-          if (s_y > zero) s.zwt = s.zwt - qcl / s_y / 1000.0f;
+          if (s_y > zero) s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
           qcharge_tot = qcharge_tot - qcl;
           if (qcharge_tot <= zero) active = false;
         }
@@ -575,14 +623,14 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
           qcl = MINF(qcl, zero);
           qcharge_tot = qcharge_tot - qcl;
           if (qcharge_tot >= zero) {
-            s.zwt = s.zwt - qcl / s_y / 1000.0f;
+            s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
             active = false;
           } else {
             s.zwt = g.zi(i) / 1000.0f;
           }
         }
       }
-      if (qcharge_tot > zero) s.zwt = s.zwt - qcharge_tot / 1000.0f / rous;
+      if (qcharge_tot > zero) s.zwt = s.zwt - m.div(qcharge_tot, 1000.0f, r1000) / rous;
     }
     jwt2 = jwt_of<L>(s.zwt, zim);
   }
@@ -603,7 +651,7 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
   int jwt3 = jwt2;
   if (jwt2 == L) {
     s.wa = s.wa - rsub_top * dt;
-    s.zwt = s.zwt + (rsub_top * dt) / 1000.0f / rous;
+    s.zwt = s.zwt + m.div(rsub_top * dt, 1000.0f, r1000) / rous;
     h2o[L] = h2o[L] + MAXF(0.0f, (s.wa - 5000.0f));
     s.wa = MINF(s.wa, 5000.0f);
   } else {
@@ -619,14 +667,14 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
         h2o[i] = h2o[i] + rstl;
         rsub_top_tot = rsub_top_tot - rstl;
         if (rsub_top_tot >= zero) {
-          s.zwt = s.zwt - rstl / s_y / 1000.0f;
+          s.zwt = s.zwt - m.div(rstl / s_y, 1000.0f, r1000);
           active = false;
         } else {
           s.zwt = g.zi(i) / 1000.0f;
         }
       }
     }
-    s.zwt = s.zwt - rsub_top_tot / 1000.0f / rous;
+    s.zwt = s.zwt - m.div(rsub_top_tot, 1000.0f, r1000) / rous;
     s.wa = s.wa + rsub_top_tot;
     jwt3 = jwt_of<L>(s.zwt, zim);
   }
@@ -645,14 +693,14 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
   // :1144-1152
   const float xs1 = MAXF(MAXF(h2o[1], zero) - cs.get(Y::TSDZ1), zero);
   h2o[1] = MINF(cs.get(Y::TSDZ1), h2o[1]);
-  const float qflx_rsub_sat = xs1 / dt;
+  const float qflx_rsub_sat = m.div(xs1, dt, g.rdt());
   // :1161-1174 watmin top-down
 #pragma unroll
   for (int i = 1; i <= L - 1; i++) {
     float xs = zero;
     if (h2o[i] < watmin) {
       xs = watmin - h2o[i];
-      if (i == jwt3) s.zwt = s.zwt + xs / MAXF(0.01f, TS(i)) / 1000.0f;
+      if (i == jwt3) s.zwt = s.zwt + m.div(xs / MAXF(0.01f, TS(i)), 1000.0f, r1000);
     }
     h2o[i] = h2o[i] + xs;
     h2o[i + 1] = h2o[i + 1] - xs;
@@ -680,13 +728,13 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
     }
   }
   h2o[L] = h2o[L] + xs;
-  rsub_top = rsub_top - xs / dt;
+  rsub_top = rsub_top - m.div(xs, dt, g.rdt());
   // :1221-1236
   float w1 = ((1.0f - frac_h2osfc) * (qflx_surf + evg + tran) + rsub_top + qflx_rsub_sat) * dt + s.wa;
 #pragma unroll
   for (int i = 1; i <= L; i++) {
     w1 = w1 + h2o[i];
-    theta[i] = MAXF(h2o[i], 1.0E-6f) / g.thk(i);
+    theta[i] = m.div(MAXF(h2o[i], 1.0E-6f), g.thk(i), g.rthk(i));
   }
   // :1244
   if (absf(w1 - w0) > 0.1f) { errval = w1 - w0; return 4; }

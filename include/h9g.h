@@ -153,6 +153,11 @@ const char *h9g_kernel_name(h9g_ctx *ctx);
 /* out[i] = expf(x[i]) if y == NULL, else powf(x[i], y[i]), on device. */
 int h9g_math_selftest(int device, int n, const float *x, const float *y,
                       float *out);
+/* out[i] = x[i]/d[i] through the kernel's fast exact division (double
+ * reciprocal); flag[i] = 1 where it defers to the exact path
+ * (subnormal quotient). */
+int h9g_div_selftest(int device, int n, const float *x, const float *d,
+                     float *out, int *flag);
 
 #ifdef __cplusplus
 }

@@ -55,3 +55,42 @@ def test_device_math_matches_glibc():
     assert same_bits(out, glibc_expf(x))
     assert lb.h9g_math_selftest(0, x.size, h._fp(x), h._fp(y), h._fp(out)) == 0
     assert same_bits(out, glibc_powf(x, y))
+
+
+def div_inputs(n=1 << 22, seed=5):
+    """Dividends/divisors over the whole float range plus the cases that
+    stress a reciprocal-based division: divisors near powers of two,
+    quotients near 1, in the subnormal range and near overflow."""
+    rng = np.random.default_rng(seed)
+    bits = lambda k: rng.integers(0, 1 << 32, k, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    x, d = bits(n), bits(n)
+    k = n // 8
+    x[:k] = rng.uniform(-1e4, 1e4, k).astype(np.float32)            # physical magnitudes
+    d[:k] = rng.uniform(-1e5, 1e5, k).astype(np.float32)
+    d[k:2 * k] = np.ldexp(1.0 + rng.integers(-4, 5, k) * 2.0 ** -23,
+                          rng.integers(-20, 20, k)).astype(np.float32)
+    x[2 * k:3 * k] = np.clip(d[2 * k:3 * k].astype(np.float64) * (1.0 + rng.uniform(-1e-6, 1e-6, k)),
+                             -3e38, 3e38).astype(np.float32)
+    x[3 * k:4 * k] = np.ldexp(rng.uniform(1, 2, k), rng.integers(-149, -100, k)).astype(np.float32)
+    ok = np.isfinite(x) & np.isfinite(d) & (d != 0)
+    return x[ok], d[ok]
+
+
+@pytest.mark.gpu
+def test_device_fast_division_is_correctly_rounded():
+    """MathFast::div with the device reciprocal equals IEEE x/d bit for bit
+    wherever it does not defer, and defers exactly on subnormal quotients."""
+    import ctypes as C
+    import hybrid9_amd as h
+    x, d = div_inputs()
+    out = np.empty_like(x)
+    flag = np.empty(x.size, np.int32)
+    rc = h.lib().h9g_div_selftest(0, x.size, h._fp(x), h._fp(d), h._fp(out),
+                                  flag.ctypes.data_as(C.POINTER(C.c_int)))
+    assert rc == 0
+    with np.errstate(all="ignore"):
+        ref = x / d
+    sub = (ref != 0) & (np.abs(ref) < np.float32(2.0 ** -126))
+    assert np.array_equal(flag.astype(bool), sub | ((out != 0) & (np.abs(out) < np.float32(2.0 ** -126))))
+    keep = flag == 0
+    assert same_bits(out[keep], ref[keep])
