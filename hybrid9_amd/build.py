@@ -18,6 +18,7 @@ HERE = Path(__file__).resolve().parent
 SRC = HERE / "csrc" / "h9g.hip"
 DEPS = [SRC, HERE / "csrc" / "h9_math.h", HERE / "csrc" / "h9g_step.h",
         HERE / "csrc" / "h9g_synth.h", HERE / "csrc" / "h9g_geo.h",
+        HERE / "csrc" / "h9g_pair.h",
         HERE.parent / "include" / "h9g.h"]
 OUT = HERE / "lib" / "libh9g.so"
 ARCH = os.environ.get("H9G_ARCH", "gfx950")

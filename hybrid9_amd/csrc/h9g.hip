@@ -30,6 +30,7 @@
 #include "h9_math.h"
 #include "h9g_geo.h"
 #include "h9g_step.h"
+#include "h9g_pair.h"
 #include "h9g_synth.h"
 
 using namespace h9k;
@@ -41,6 +42,11 @@ static const double h_log2tab[32] = H9M_POWF_LOG2_TAB_INIT;
 
 #define H9G_BLOCK 256
 #define H9G_YBLOCK 64   // year kernel: one wave per block (LDS cell stores)
+// pair kernel: 22 columns (44 lanes) per wave, 4 waves per workgroup; the
+// 0.5 deg grid is 767 workgroups = 3 waves on each of the 1,024 SIMDs
+#define H9G_PCPW 22
+#define H9G_PLANES (2 * H9G_PCPW)
+#define H9G_PWAVES 4
 #define NEVT 64
 
 // ---------------------------------------------------------------------------
@@ -145,6 +151,97 @@ __global__ void __launch_bounds__(H9G_YBLOCK) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + cw] = __builtin_nanf("");
     return;
+  }
+}
+
+// Pair kernel (h9g_pair.h): two lanes per soil column, the per-layer powers
+// split over the pair.  Same arguments, layouts and results as
+// h9g_year_kernel.
+template <int L, class G>
+__global__ void __launch_bounds__(64 * H9G_PWAVES) __attribute__((amdgpu_waves_per_eu(3, 3)))
+h9g_pair_kernel(const KArgs a, const G g) {
+  typedef PairStore<L, H9G_PLANES> PS;
+  __shared__ uint64_t s_e2[32];
+  __shared__ double s_l2[32];
+  __shared__ float s_cell[H9G_PWAVES][PS::ROWS * H9G_PLANES];   // [wave][row][lane]
+  load_tabs(s_e2, s_l2);
+  const h9m::Tabs T = {s_e2, s_l2};
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane >= H9G_PLANES) return;
+  const int h = lane & 1;
+  const int c = (blockIdx.x * H9G_PWAVES + wave) * H9G_PCPW + (lane >> 1);
+  if (c >= a.ncell) return;          // both lanes of a pair leave together
+  const int n = a.ncell;
+
+  PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1]};
+  const Split2 sp{h};
+  St<L> s;
+#pragma unroll
+  for (int p = 0; p < 4; p++)
+#pragma unroll
+    for (int t = 0; t < L / 2; t++) cs.set_slot(p, t, a.par[(size_t)(p * L + 2 * t + h) * n + c]);
+  cs.set_sc(PS_FMAX, a.par[(size_t)(4 * L) * n + c]);
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    s.h2o[i] = a.st[(size_t)(0 * L + i - 1) * n + c];
+    s.smp[i] = a.st[(size_t)(2 * L + i - 1) * n + c];
+  }
+#pragma unroll
+  for (int t = 0; t < L / 2; t++) cs.set_slot(PF_ROOTR, t, a.st[(size_t)(3 * L + 2 * t + h) * n + c]);
+  const size_t o8 = (size_t)(4 * L + 1) * n + c;
+  s.zwt = a.st[o8 + 0 * (size_t)n];
+  s.wa = a.st[o8 + 1 * (size_t)n];
+  s.LAI = a.st[o8 + 2 * (size_t)n];
+  s.LAI_litter = a.st[o8 + 3 * (size_t)n];
+  s.pm = a.st[o8 + 4 * (size_t)n];
+  s.pfm = a.st[o8 + 5 * (size_t)n];
+  s.plen = a.st[o8 + 6 * (size_t)n];
+  s.rdepth = a.st[o8 + 7 * (size_t)n];
+  cs.launder();
+
+  // soil mask (HYBRID9.f90:122-123): SUM(theta_s) > trunc
+  float ts_sum = zero;
+#pragma unroll
+  for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.lay(PF_TS, i);
+  if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
+    if (h == 0)
+#pragma unroll
+      for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + c] = __builtin_nanf("");
+    return;
+  }
+  cell_inv_pair<L, G>(g, cs);
+  int eday = 0, estep = 0;
+  float errval = 0.0f;
+  const int code = cell_year_pair<L, G>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar, a.nt, a.nisurf,
+                                        a.grow_on, a.annual + c, (size_t)n, eday, estep, errval, T);
+  if (h != 0) return;                // the even lane writes the cell back
+  int cw = c;
+  opaque(cw);
+  cs.launder();
+  const size_t ow = (size_t)(4 * L + 1) * n + cw;
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    a.st[(size_t)(0 * L + i - 1) * n + cw] = s.h2o[i];
+    a.st[(size_t)(2 * L + i - 1) * n + cw] = s.smp[i];
+    if (a.grow_on) a.st[(size_t)(3 * L + i - 1) * n + cw] = cs.lay(PF_ROOTR, i);
+  }
+  if (a.grow_on) a.st[(size_t)(4 * L) * n + cw] = zero;   // rootr_col(Nlevgrnd)
+  a.st[ow + 0 * (size_t)n] = s.zwt;
+  a.st[ow + 1 * (size_t)n] = s.wa;
+  a.st[ow + 2 * (size_t)n] = s.LAI;
+  a.st[ow + 3 * (size_t)n] = s.LAI_litter;
+  a.st[ow + 4 * (size_t)n] = s.pm;
+  a.st[ow + 5 * (size_t)n] = s.pfm;
+  a.st[ow + 6 * (size_t)n] = s.plen;
+  a.st[ow + 7 * (size_t)n] = s.rdepth;
+  if (code) {
+    a.err[0 * (size_t)n + cw] = code;
+    a.err[1 * (size_t)n + cw] = eday;
+    a.err[2 * (size_t)n + cw] = estep;
+    a.err[3 * (size_t)n + cw] = __builtin_bit_cast(int, errval);
+    atomicOr(a.err_flag, 1);
+#pragma unroll
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + cw] = __builtin_nanf("");
   }
 }
 
@@ -295,6 +392,7 @@ struct h9g_ctx {
   int params_set = 0, state_set = 0, ran = 0;
   h9g_error last_err{};
   const char *kname = "";
+  int pair = 1;        // 1: h9g_pair_kernel (default), 0: h9g_year_kernel (H9G_KERNEL=single)
 };
 
 #define HIPCHK(x)                                                              \
@@ -433,12 +531,15 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     h9g_destroy(ctx);
     return nullptr;
   }
-  static const char *names[2][3] = {{"h9g_year_kernel<8,GeoR>", "h9g_year_kernel<8,GeoC<8,24>>",
-                                     "h9g_year_kernel<8,GeoC<8,48>>"},
-                                    {"h9g_year_kernel<10,GeoR>", "h9g_year_kernel<10,GeoC<10,24>>",
-                                     "h9g_year_kernel<10,GeoC<10,48>>"}};
+  static const char *names[2][2][3] = {
+      {{"h9g_year_kernel<8,GeoR>", "h9g_year_kernel<8,GeoC<8,24>>", "h9g_year_kernel<8,GeoC<8,48>>"},
+       {"h9g_year_kernel<10,GeoR>", "h9g_year_kernel<10,GeoC<10,24>>", "h9g_year_kernel<10,GeoC<10,48>>"}},
+      {{"h9g_pair_kernel<8,GeoR>", "h9g_pair_kernel<8,GeoC<8,24>>", "h9g_pair_kernel<8,GeoC<8,48>>"},
+       {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}}};
+  const char *kenv = getenv("H9G_KERNEL");
+  ctx->pair = !(kenv && strcmp(kenv, "single") == 0);
   const GeoKind gk = geo_kind(*cfg);
-  ctx->kname = names[L == 8 ? 0 : 1][gk == GEO_R ? 0 : (gk == GEO_C24 ? 1 : 2)];
+  ctx->kname = names[ctx->pair][L == 8 ? 0 : 1][gk == GEO_R ? 0 : (gk == GEO_C24 ? 1 : 2)];
   return ctx;
 }
 
@@ -594,8 +695,14 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   }
   const int e = ctx->nev++;
   HIPCHK(hipEventRecord(ctx->ev0[e], ctx->sc));
-  H9G_DISPATCH(ctx, h9g_year_kernel, (unsigned)((ctx->n + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
-               ctx->sc, a);
+  if (ctx->pair) {
+    const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
+    H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n + per_block - 1) / per_block), 64 * H9G_PWAVES,
+                 ctx->sc, a);
+  } else {
+    H9G_DISPATCH(ctx, h9g_year_kernel, (unsigned)((ctx->n + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
+                 ctx->sc, a);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1[e], ctx->sc));
   HIPCHK(hipEventRecord(ctx->ev_consumed[slot], ctx->sc));

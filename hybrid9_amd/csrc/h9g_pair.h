@@ -1,0 +1,821 @@
+// h9g_pair.h -- HYDROLOGY substep with two lanes per soil column.
+//
+// Why: the 0.5 deg grid has 67,420 land cells, i.e. 1,054 one-lane waves
+// for 1,024 SIMDs.  One wave per SIMD leaves VALU issue and LDS latency
+// exposed (a lone wave64 issues at most every 4 cycles; the SIMD can take
+// one every 2), and the 30 surplus waves double up on 30 SIMDs and set the
+// kernel time.  Giving each column two lanes ("a pair": lanes 2k, 2k+1 of
+// a wave) halves the per-lane share of the work that is independent per
+// layer -- the equilibrium profile zq (HYDROLOGY.f90:517-590), hydraulic
+// conductivity and matric potential (:598-639) and the specific yields
+// (:937-981), i.e. 40 of the ~46 glibc-exact powf of a substep -- and
+// lets 22 columns per wave x 4-wave workgroups place exactly 3 waves on
+// every SIMD (767 workgroups for 768 slots at 0.5 deg).
+//
+// Layer split: lane h (0 = even, 1 = odd) of a pair owns layers 2t+1+h,
+// t = 0..L/2-1.  A per-layer phase evaluates the reference expression for
+// the lane's own layers and swaps the results with the partner lane (DPP
+// quad_perm [1,0,3,2]); everything else (energy balance, tridiagonal
+// system, Thomas solve, drainage, ...) runs identically in both lanes.
+// Every value is computed by exactly the reference expression, so the
+// split changes no bit.
+//
+// One code path serves three builds through two policies:
+//   Split2   device fast path: own layers per lane + DPP exchange;
+//   SplitAll one lane computes every layer: the device exact re-run
+//            (MathExact) and the host test build (tests/csrc/host_kernel.cpp).
+// Stores: PairStore (device LDS, [row][lane] with the pair's layers
+// interleaved over its two columns) and FlatStore (host, flat per cell).
+#pragma once
+#include "h9g_step.h"
+#if !defined(__HIPCC__) && !defined(__HIP__)
+#define __device__
+#define __forceinline__ inline
+#endif
+
+namespace h9k {
+
+// per-layer store fields (L entries each)
+enum : int {
+  PF_TS = 0, PF_HKS, PF_BSW, PF_PSI,   // soil parameters (SHARED.f90:398-429)
+  PF_NINVB,                            // -one/bsw
+  PF_ITS,                              // one/(ts(I)+ts(I+1))
+  PF_PTE,                              // psi*ts/(one-one/bsw)
+  PF_C3,                               // pte/(zi(I)-zi(I-1))
+  PF_ROOTR,                            // rootr_col(1..L)
+  PF_SVH2O, PF_SVSMP,                  // substep rollback
+  PF_N
+};
+// per-cell fields
+enum : int {
+  PS_FMAX = 0, PS_MH3, PS_TSDZ1, PS_SVZWT, PS_SVWA, PS_SVRNF, PS_SVERR, PS_DAY,
+  PS_N = PS_DAY + D_N
+};
+
+template <int K>
+struct FV {
+  float v[K];
+};
+
+H9K_HD float sel(int h, float a, float b) { return h ? b : a; }
+H9K_HD double seld(int h, double a, double b) { return h ? b : a; }
+
+// value of the partner lane (lane ^ 1)
+H9K_HD float pair_swap(float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int x = __builtin_bit_cast(int, v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false));
+#else
+  return v;
+#endif
+}
+
+// ------------------------------------------------------------------ stores
+template <int L>
+struct FlatStore {                     // host: one flat array per cell
+  static constexpr int N = PF_N * L + PS_N;
+  float *b;
+  H9K_HD float lay(int p, int i) const { return b[p * L + i - 1]; }
+  H9K_HD void set_lay(int p, int i, float v) const { b[p * L + i - 1] = v; }
+  H9K_HD float sc(int k) const { return b[PF_N * L + k]; }
+  H9K_HD void set_sc(int k, float v) const { b[PF_N * L + k] = v; }
+  H9K_HD float slot(int p, int t) const { return b[p * L + 2 * t]; }   // unused (SplitAll)
+  H9K_HD void set_slot(int p, int t, float v) const { b[p * L + 2 * t] = v; }
+  H9K_HD void launder() {}
+  H9K_HD float day(int f) const { return sc(PS_DAY + f); }
+  H9K_HD void set_day(int f, float v) const { set_sc(PS_DAY + f, v); }
+  H9K_HD float root(int i) const { return lay(PF_ROOTR, i); }
+  H9K_HD void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
+};
+
+// Device: [row][S] LDS block per wave, S = lanes per wave.  Layer i of a
+// per-layer field sits in row p*L/2 + (i-1)/2 of the pair's column
+// (i-1)&1, so a lane's own layers are its own column's rows and any layer
+// is a static offset from the pair's even column.  Per-cell fields are
+// spread the same way over the two columns.  Both lanes of a pair store
+// identical values to the same address where they both write.
+template <int L, int S>
+struct PairStore {
+  static constexpr int NT = L / 2;
+  static constexpr int ROWS = PF_N * NT + (PS_N + 1) / 2;
+  lds_float *self, *even;
+  __device__ __forceinline__ float lay(int p, int i) const {
+    return even[(p * NT + ((i - 1) >> 1)) * S + ((i - 1) & 1)];
+  }
+  __device__ __forceinline__ void set_lay(int p, int i, float v) const {
+    even[(p * NT + ((i - 1) >> 1)) * S + ((i - 1) & 1)] = v;
+  }
+  __device__ __forceinline__ float sc(int k) const { return even[(PF_N * NT + (k >> 1)) * S + (k & 1)]; }
+  __device__ __forceinline__ void set_sc(int k, float v) const {
+    even[(PF_N * NT + (k >> 1)) * S + (k & 1)] = v;
+  }
+  __device__ __forceinline__ float slot(int p, int t) const { return self[(p * NT + t) * S]; }
+  __device__ __forceinline__ void set_slot(int p, int t, float v) const { self[(p * NT + t) * S] = v; }
+  __device__ __forceinline__ void launder() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(self), "+v"(even)::"memory");
+#endif
+  }
+  __device__ __forceinline__ float day(int f) const { return sc(PS_DAY + f); }
+  __device__ __forceinline__ void set_day(int f, float v) const { set_sc(PS_DAY + f, v); }
+  __device__ __forceinline__ float root(int i) const { return lay(PF_ROOTR, i); }
+  __device__ __forceinline__ void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
+};
+
+// ---------------------------------------------------------------- policies
+// One lane computes every layer.
+struct SplitAll {
+  template <class CS>
+  H9K_HD float own(const CS &cs, int p, int t, int h) const { return cs.lay(p, 2 * t + 1 + h); }
+  // out[2t+1+h] = f(t, h).f for every layer; K outputs per layer
+  template <int NT, int K, class F>
+  H9K_HD void par(F f, float *const (&out)[K]) const {
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const FV<K> r = f(t, h);
+#pragma unroll
+        for (int k = 0; k < K; k++) out[k][2 * t + 1 + h] = r.v[k];
+      }
+      sched_fence();
+    }
+  }
+  // r0 = f(0), r1 = f(1)
+  template <int K, class F>
+  H9K_HD void pick(F f, FV<K> &r0, FV<K> &r1) const {
+    r0 = f(0);
+    r1 = f(1);
+  }
+  H9K_HD bool pair_any(bool p) const { return p; }
+};
+
+// Two lanes per column (device fast path); h = lane & 1.
+struct Split2 {
+  int h;
+  template <class CS>
+  H9K_HD float own(const CS &cs, int p, int t, int) const { return cs.slot(p, t); }
+  template <int NT, int K, class F>
+  H9K_HD void par(F f, float *const (&out)[K]) const {
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      const FV<K> r = f(t, h);
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const float o = pair_swap(r.v[k]);
+        out[k][2 * t + 1] = sel(h, r.v[k], o);
+        out[k][2 * t + 2] = sel(h, o, r.v[k]);
+      }
+      sched_fence();
+    }
+  }
+  template <int K, class F>
+  H9K_HD void pick(F f, FV<K> &r0, FV<K> &r1) const {
+    const FV<K> r = f(h);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const float o = pair_swap(r.v[k]);
+      r0.v[k] = sel(h, r.v[k], o);
+      r1.v[k] = sel(h, o, r.v[k]);
+    }
+  }
+  H9K_HD bool pair_any(bool p) const {
+    const float f = p ? 1.0f : 0.0f;
+    return (f + pair_swap(f)) != 0.0f;
+  }
+};
+
+// Rollback copy of a per-layer state array (1-based v[1..L]).
+template <int L, class CS>
+H9K_HD void save_layers(const SplitAll &, const CS &cs, int p, const float *v) {
+#pragma unroll
+  for (int i = 1; i <= L; i++) cs.set_lay(p, i, v[i]);
+}
+template <int L, class CS>
+H9K_HD void save_layers(const Split2 &sp, const CS &cs, int p, const float *v) {
+#pragma unroll
+  for (int t = 0; t < L / 2; t++) cs.set_slot(p, t, sel(sp.h, v[2 * t + 1], v[2 * t + 2]));
+}
+
+// Parameter-only invariants (as cell_inv), into a pair/flat store.
+template <int L, class G, class CS>
+H9K_HD void cell_inv_pair(const G &g, const CS &cs) {
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    const int ip = (L < i + 1) ? L : i + 1;
+    const float ts = cs.lay(PF_TS, i), tsp = cs.lay(PF_TS, ip);
+    const float bsw = cs.lay(PF_BSW, i), psi = cs.lay(PF_PSI, i);
+    const float e = one - one / bsw;
+    cs.set_lay(PF_NINVB, i, -one / bsw);
+    cs.set_lay(PF_ITS, i, one / (ts + tsp));
+    const float pte = psi * ts / e;
+    cs.set_lay(PF_PTE, i, pte);
+    cs.set_lay(PF_C3, i, pte / (g.zi(i) - g.zi(i - 1)));
+  }
+  float mh = cs.lay(PF_HKS, 1);
+  if (cs.lay(PF_HKS, 2) < mh) mh = cs.lay(PF_HKS, 2);
+  if (cs.lay(PF_HKS, 3) < mh) mh = cs.lay(PF_HKS, 3);
+  cs.set_sc(PS_MH3, mh);
+  cs.set_sc(PS_TSDZ1, MAXF(zero, (cs.lay(PF_TS, 1) * g.dz(1))));
+}
+
+// One HYDROLOGY call (HYDROLOGY.f90:141-1283), pair-split.  Same contract
+// as hydrology_step (h9g_step.h), whose comments cite each block.
+template <int L, class G, class M, class SP, class CS>
+H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta,
+                          float &rnf_sum, float &errval, M &m) {
+  constexpr int NT = L / 2;
+  const float dt = g.dt();
+  constexpr double r1000 = 1.0 / 1000.0;
+  float zim[L + 1];
+#pragma unroll
+  for (int i = 1; i <= L; i++) zim[i] = g.zim(i);
+  float *h2o = s.h2o, *smp = s.smp;
+  cs.launder();
+#define TS(i) cs.lay(PF_TS, i)
+#define HKS(i) cs.lay(PF_HKS, i)
+#define BSW(i) cs.lay(PF_BSW, i)
+#define PSI(i) cs.lay(PF_PSI, i)
+#define LAYF(F, i) cs.lay(F, i)
+#define ROOT(i) cs.lay(PF_ROOTR, i)
+#define DC(F) cs.sc(PS_DAY + F)
+#define OWN(p) sp.own(cs, p, t, h)
+
+  // :141-151
+  float w0 = DC(D_FORC) * dt + s.wa;
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    w0 = w0 + h2o[i];
+    theta[i] = m.div(h2o[i], g.thk(i), g.rthk(i));
+  }
+  // :161-212
+  const float qflx_top_soil = DC(D_FORC);
+  const float hkdepth = one / 2.5f;
+  const float fff = 1.0f / hkdepth;
+  const float fsat = cs.sc(PS_FMAX) * m.expf(-0.5f * fff * s.zwt);
+  float qflx_surf = fsat * qflx_top_soil;
+  const float frac_h2osfc = zero;
+  // :269-276 (previous-step smp)
+  float beta = zero;
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    float b = one - m.div(smp[i] - g.zc(i), -150000.0f, 1.0 / -150000.0);
+    b = MINF(one, b);
+    b = MAXF(zero, b);
+    beta = beta + ROOT(i) * b;
+  }
+  // :283-295
+  float rsc;
+  if ((DC(D_OK) != zero) && (beta > zero))
+    rsc = DC(D_X) / (DC(D_LAI2) * beta * DC(D_PW28));
+  else
+    rsc = 1.0E6f;
+  rsc = MAXF(rsc, DC(D_RSCMIN));
+  // :325-331
+  float rss;
+  if (theta[1] <= 0.15f)
+    rss = DC(D_LIT) * m.expf(0.3563f * 100.0f * (0.15f - theta[1]));
+  else
+    rss = (10.0f + DC(D_LIT1000) * (1.0f - theta[1] / TS(1)));
+  // :344-389
+  const float desatdT = DC(D_DESAT), gamma = DC(D_GAMMA);
+  const float PMc = DC(D_NUMC) / (desatdT + gamma * (one + rsc / DC(D_RAARAC)));
+  const float PMs = DC(D_NUMS) / (desatdT + gamma * (one + rss / DC(D_RAARAS)));
+  const float Ra = DC(D_RA);
+  const float Rs = DC(D_DGRAS) + gamma * rss;
+  const float Rc = DC(D_DGRAC) + gamma * rsc;
+  const float Cc = one / (one + Rc * Ra / (Rs * (Rc + Ra)));
+  const float Cs = one / (one + Rs * Ra / (Rc * (Rs + Ra)));
+  const float LE = Cc * PMc + Cs * PMs;
+  const float VDD0 = DC(D_VDD) + (DC(D_A1) - DC(D_DG) * LE) * DC(D_RAA) / DC(D_RHOCP);
+  const float LEc = (DC(D_DRR) + DC(D_RHOCP) * VDD0 / DC(D_RAC)) / (desatdT + gamma * (1.0f + rsc / DC(D_RAC)));
+  const float LEs = (DC(D_DRG) + DC(D_RHOCP) * VDD0 / DC(D_RAS)) / (desatdT + gamma * (1.0f + rss / DC(D_RAS)));
+  const float tran = LEc * 1.0E3f / DC(D_RL);
+  float evg = LEs * 1.0E3f / DC(D_RL);
+  // :396-400
+  float em1 = m.div(g.dz(1) * (theta[1] - watmin), dt, g.rdt()) - tran * ROOT(1);
+  em1 = MAXF(zero, em1);
+  evg = MINF(em1, evg);
+  // :426-478
+  const float qflx_evap = evg;
+  float qflx_in_soil = (one - frac_h2osfc) * (qflx_top_soil - qflx_surf);
+  qflx_in_soil = qflx_in_soil - (one - frac_h2osfc) * qflx_evap;
+  const float qinmax = (one - fsat) * cs.sc(PS_MH3);
+  const float qflx_infl_excess = MAXF(zero, qflx_in_soil - (one - frac_h2osfc) * qinmax);
+  const float qflx_infl = qflx_in_soil - qflx_infl_excess;
+  qflx_surf = qflx_surf + qflx_infl_excess;
+  // :492-508
+  float zwtmm = 1000.0f * s.zwt;
+  const int jwt = jwt_of<L>(s.zwt, zim);
+  const bool aq = (jwt == L);
+  cs.launder();
+
+  // :517-567 equilibrium profile, own layers
+  float zq[L + 2];
+  {
+    float *const out[1] = {zq};
+    sp.template par<NT, 1>(
+        [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
+          const int i0 = 2 * t + 1;                           // own layer i = i0 + h
+          const float zlo = sel(h, g.zi(i0 - 1), g.zi(i0));   // zi(i-1)
+          const float zhi = sel(h, g.zi(i0), g.zi(i0 + 1));   // zi(i)
+          const float ts = OWN(PF_TS), psi = OWN(PF_PSI);
+          float vol_eq;
+          if (zwtmm <= zlo) {
+            vol_eq = ts;
+          } else {
+            const float expo = one + OWN(PF_NINVB);
+            const float temp0 = m.powf((((-psi) + zwtmm - zlo) / (-psi)), expo);
+            if ((zwtmm < zhi) && (zwtmm > zlo)) {
+              const float tempi = one;
+              const float voleq1 = OWN(PF_PTE) / (zwtmm - zlo) * (tempi - temp0);
+              vol_eq = m.div(voleq1 * (zwtmm - zlo) + ts * (zhi - zwtmm), sel(h, g.dz(i0), g.dz(i0 + 1)),
+                             seld(h, g.rdz(i0), g.rdz(i0 + 1)));
+              vol_eq = MINF(ts, vol_eq);
+              vol_eq = MAXF(vol_eq, zero);
+            } else {
+              const float tempi = m.powf(((-psi + zwtmm - zhi) / (-psi)), expo);
+              vol_eq = OWN(PF_C3) * (tempi - temp0);
+              vol_eq = MAXF(vol_eq, 0.0f);
+              vol_eq = MINF(ts, vol_eq);
+            }
+          }
+          float z = psi * m.powf(MAXF(vol_eq / ts, 0.01f), -OWN(PF_BSW));
+          return FV<1>{{MAXF(smpmin, z)}};
+        },
+        out);
+  }
+  // Four single powers split over the pair (unused ones get base 1):
+  //   lane 0: temp0 of the aquifer node (:579-580), then zq(L+1) (:581-590);
+  //   lane 1: the specific-yield power of layer L (:937-940), then smp1 of
+  //           the aquifer row (:737-741).
+  FV<1> pA, pY;
+  sp.template pick<1>(
+      [&](int h) __attribute__((always_inline)) -> FV<1> {
+        const float npsi = -PSI(L);
+        const float num = sel(h, aq ? (-PSI(L) + zwtmm - g.zi(L)) : npsi, zwtmm);
+        const float q = num / npsi;
+        const float ninv = LAYF(PF_NINVB, L);
+        return FV<1>{{m.powf(sel(h, q, one + q), sel(h, one + ninv, ninv))}};
+      },
+      pA, pY);
+  FV<2> eA, eS;
+  {
+    const float d0 = aq ? (zwtmm - g.zi(L)) : one;
+    float ve = LAYF(PF_PTE, L) / d0 * (1.0f - pA.v[0]);
+    ve = MAXF(ve, 0.0f);
+    ve = MINF(TS(L), ve);
+    sp.template pick<2>(
+        [&](int h) __attribute__((always_inline)) -> FV<2> {
+          const float q2 = sel(h, ve, theta[L]) / TS(L);
+          float sn = MAXF(0.5f * (one + q2), 0.01f);
+          sn = MINF(one, sn);
+          float x = sel(h, MAXF(q2, 0.01f), sn);
+          if (!aq) x = one;
+          float z = PSI(L) * m.powf(x, -BSW(L));
+          z = MAXF(smpmin, z);
+          return FV<2>{{z, -BSW(L) * z / (x * TS(L))}};
+        },
+        eA, eS);
+  }
+  zq[L + 1] = aq ? eA.v[0] : zero;
+  const float smp1 = eS.v[0], dsmpdw1 = eS.v[1];
+  cs.launder();
+
+  // :598-639 conductivity and matric potential, own layers
+  float hk[L + 1], dhkdw[L + 1], dsmpdw[L + 1];
+  {
+    float *const out[4] = {hk, dhkdw, smp, dsmpdw};
+    sp.template par<NT, 4>(
+        [&](int t, int h) __attribute__((always_inline)) -> FV<4> {
+          const int i0 = 2 * t + 1;
+          const int ip1 = (L < i0 + 2) ? L : i0 + 2;          // ip of layer i0+1
+          const float th = sel(h, theta[i0], theta[i0 + 1]);
+          const float thp = sel(h, theta[i0 + 1], theta[ip1]);
+          const float ts = OWN(PF_TS);
+          const float tsp = sel(h, TS(i0 + 1), TS(ip1));
+          float s1 = 0.5f * (th + thp) / (0.5f * (ts + tsp));
+          s1 = MINF(one, s1);
+          const float bsw = OWN(PF_BSW);
+          const float s2 = OWN(PF_HKS) * m.powf(s1, 2.0f * bsw + 2.0f);
+          FV<4> r;
+          r.v[0] = s1 * s2;
+          r.v[1] = (2.0f * bsw + 3.0f) * s2 * OWN(PF_ITS);
+          float s_node = MAXF(th / ts, 0.01f);
+          s_node = MINF(one, s_node);
+          float sm = OWN(PF_PSI) * m.powf(s_node, -bsw);
+          sm = MAXF(smpmin, sm);
+          r.v[2] = sm;
+          r.v[3] = (-bsw) * sm / (s_node * ts);
+          return r;
+        },
+        out);
+  }
+  // :645-650 aquifer node geometry
+  const float zcA = 0.5f * (zwtmm + g.zc(L));
+  const float dzA = (jwt < L) ? g.dz(L) : zwtmm - g.zc(L);
+  cs.launder();
+  // Tridiagonal system rows 1..L+1 (:661-799), each row eliminated as soon
+  // as it is assembled (Thomas forward sweep, :806-831).  The flux terms
+  // of interface k are the reference's qout/dqodw1/dqodw2 of row k and,
+  // bit for bit the same expressions, qin/dqidw0/dqidw1 of row k+1; they
+  // are evaluated once.
+  float dwat2[L + 2], GAM[L + 2];
+  float BET = zero, cprev = zero;
+  double rbet = 0.0;
+  int zero_pivot = 0;
+  auto row = [&](int i, float am, float bm, float cm, float rm) __attribute__((always_inline)) {
+    if (i == 1) {
+      BET = bm;
+      rbet = recip64(BET);
+      dwat2[1] = m.div(rm, BET, rbet);
+    } else {
+      GAM[i] = m.div(cprev, BET, rbet);
+      BET = bm - am * GAM[i];
+      if (BET == 0.0f && !zero_pivot) zero_pivot = i;
+      rbet = recip64(BET);
+      dwat2[i] = m.div(rm - am * dwat2[i - 1], BET, rbet);
+    }
+    cprev = cm;
+  };
+  float q_prev, dq0_prev, dq1_prev;      // interface i-1
+  {
+    const float den = g.den(1);
+    const double rden = g.rden(1);
+    const float dzq = (zq[2] - zq[1]);
+    const float num = (smp[2] - smp[1]) - dzq;
+    const float qout = m.div(-hk[1] * num, den, rden);
+    const float dqodw1 = m.div(-(-hk[1] * dsmpdw[1] + num * dhkdw[1]), den, rden);
+    const float dqodw2 = m.div(-(hk[1] * dsmpdw[2] + num * dhkdw[1]), den, rden);
+    const float bm1 = m.div(g.dz(1), dt, g.rdt()) + dqodw1;
+    if (bm1 == 0.0f) { errval = bm1; return 1; }                    // :806-812
+    row(1, zero, bm1, dqodw2, qflx_infl - qout - tran * ROOT(1));
+    q_prev = qout; dq0_prev = dqodw1; dq1_prev = dqodw2;
+  }
+#pragma unroll
+  for (int i = 2; i <= L - 1; i++) {
+    const float den = g.den(i);
+    const double rden = g.rden(i);
+    const float dzq = zq[i + 1] - zq[i];
+    const float num = (smp[i + 1] - smp[i]) - dzq;
+    const float qout = m.div(-hk[i] * num, den, rden);
+    const float dqodw1 = m.div(-(-hk[i] * dsmpdw[i] + num * dhkdw[i]), den, rden);
+    const float dqodw2 = m.div(-(hk[i] * dsmpdw[i + 1] + num * dhkdw[i]), den, rden);
+    row(i, -dq0_prev, m.div(g.dz(i), dt, g.rdt()) - dq1_prev + dqodw1, dqodw2,
+        q_prev - qout - tran * ROOT(i));
+    q_prev = qout; dq0_prev = dqodw1; dq1_prev = dqodw2;
+  }
+  {
+    constexpr int i = L;
+    if (i > jwt) {                 // water table inside the column
+      const float qout = zero, dqodw1 = zero;
+      row(i, -dq0_prev, m.div(g.dz(i), dt, g.rdt()) - dq1_prev + dqodw1, zero,
+          q_prev - qout - tran * ROOT(i));
+      row(i + 1, zero, m.div(dzA, dt, g.rdt()), zero, zero);
+    } else {                       // below: aquifer row (smp1, dsmpdw1 from the pair split)
+      const float den = zcA - g.zc(i);
+      const double rden = recip64(den);
+      const float dzq = zq[i + 1] - zq[i];
+      const float num = smp1 - smp[i] - dzq;
+      const float qout = m.div(-hk[i] * num, den, rden);
+      const float dqodw1 = m.div(-(-hk[i] * dsmpdw[i] + num * dhkdw[i]), den, rden);
+      const float dqodw2 = m.div(-(hk[i] * dsmpdw1 + num * dhkdw[i]), den, rden);
+      row(i, -dq0_prev, m.div(g.dz(i), dt, g.rdt()) - dq1_prev + dqodw1, dqodw2,
+          q_prev - qout - tran * ROOT(i));
+      const float qout1 = zero, dqodw1b = zero;
+      row(i + 1, -dqodw1, m.div(dzA, dt, g.rdt()) - dqodw2 + dqodw1b, zero, qout - qout1);
+    }
+  }
+  if (zero_pivot) { errval = (float)zero_pivot; return 2; }          // :818-825
+#pragma unroll
+  for (int i = L; i >= 1; i--) dwat2[i] = dwat2[i] - GAM[i + 1] * dwat2[i + 1];
+  // :845-850
+#pragma unroll
+  for (int i = 1; i <= L; i++) h2o[i] = h2o[i] + dwat2[i] * g.dz(i);
+  cs.launder();
+  // :856-904 recharge
+  float qcharge;
+  if (jwt < L) {
+    float th_j = zero, ts_j = one, hks_j = zero, bsw_j = zero, smp_m = zero, zq_m = zero, zc_j = zero;
+#pragma unroll
+    for (int i = 1; i <= L; i++) {
+      if (i == jwt + 1) { th_j = theta[i]; ts_j = TS(i); hks_j = HKS(i); bsw_j = BSW(i); }
+      if (i == (jwt > 1 ? jwt : 1)) { smp_m = smp[i]; zq_m = zq[i]; }
+      if (i == jwt) zc_j = g.zc(i);
+    }
+    const float wh_zwt = zero;
+    const float s_node = MAXF(th_j / ts_j, 0.01f);
+    const float s1 = MINF(one, s_node);
+    const float ka = hks_j * m.powf(s1, 2.0f * bsw_j + 3.0f);
+    const float smp1m = MAXF(smpmin, smp_m);
+    const float wh = smp1m - zq_m;
+    if (jwt == 0)
+      qcharge = -ka * (wh_zwt - wh) / (zwtmm + one);
+    else
+      qcharge = -ka * (wh_zwt - wh) / ((zwtmm - zc_j) * 2.0f);
+    qcharge = MAXF(-10.0f / dt, qcharge);
+    qcharge = MINF(10.0f / dt, qcharge);
+  } else {
+    qcharge = m.div(dwat2[L + 1] * dzA, dt, g.rdt());
+  }
+  // :923-1009 water table from recharge; specific yields s_y(I) for the
+  // current zwtmm, all layers only if some lane has its water table inside
+  // the column (sy(L) = rous came from the pair split above)
+  float sy[L + 1];
+  sy[L] = MAXF(TS(L) * (one - pY.v[0]), 0.02f);
+  if (any_lane(jwt < L)) {
+    float *const out[1] = {sy};
+    sp.template par<NT, 1>(
+        [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
+          return FV<1>{{MAXF(OWN(PF_TS) * (one - m.powf((one + zwtmm / (-OWN(PF_PSI))), OWN(PF_NINVB))), 0.02f)}};
+        },
+        out);
+  }
+  float rous = sy[L];
+  int jwt2 = jwt;
+  if (jwt == L) {
+    s.wa = s.wa + qcharge * dt;
+    s.zwt = s.zwt - m.div(qcharge * dt, 1000.0f, r1000) / rous;
+  } else {
+    float qcharge_tot = qcharge * dt;
+    if (qcharge_tot > zero) {          // rising: I = jwt+1 .. 1
+      bool active = true;
+#pragma unroll
+      for (int i = L; i >= 1; i--) {
+        if (active && i <= jwt + 1) {
+          const float s_y = sy[i];
+          float qcl = MINF(qcharge_tot, s_y * (zwtmm - g.zi(i - 1)));
+          qcl = MAXF(qcl, zero);
+          if (s_y > zero) s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
+          qcharge_tot = qcharge_tot - qcl;
+          if (qcharge_tot <= zero) active = false;
+        }
+      }
+    } else {                            // deepening: I = jwt+1 .. L
+      bool active = true;
+#pragma unroll
+      for (int i = 1; i <= L; i++) {
+        if (active && i >= jwt + 1) {
+          const float s_y = sy[i];
+          float qcl = MAXF(qcharge_tot, -s_y * (g.zi(i) - zwtmm));
+          qcl = MINF(qcl, zero);
+          qcharge_tot = qcharge_tot - qcl;
+          if (qcharge_tot >= zero) {
+            s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
+            active = false;
+          } else {
+            s.zwt = g.zi(i) / 1000.0f;
+          }
+        }
+      }
+      if (qcharge_tot > zero) s.zwt = s.zwt - m.div(qcharge_tot, 1000.0f, r1000) / rous;
+    }
+    jwt2 = jwt_of<L>(s.zwt, zim);
+  }
+  cs.launder();
+  // :1015-1035 baseflow; s_y for the new zwtmm (:1077-1080)
+  zwtmm = 1000.0f * s.zwt;
+  float rsub_top = 5.5E-3f * m.expf(-fff * s.zwt);
+  if (any_lane(jwt2 < L)) {
+    float *const out[1] = {sy};
+    sp.template par<NT, 1>(
+        [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
+          return FV<1>{{MAXF(OWN(PF_TS) * (one - m.powf((one + zwtmm / (-OWN(PF_PSI))), OWN(PF_NINVB))), 0.02f)}};
+        },
+        out);
+  } else {
+    sy[L] = MAXF(TS(L) * (one - m.powf((one + zwtmm / (-PSI(L))), LAYF(PF_NINVB, L))), 0.02f);
+  }
+  rous = sy[L];
+  // :1048-1118
+  int jwt3 = jwt2;
+  if (jwt2 == L) {
+    s.wa = s.wa - rsub_top * dt;
+    s.zwt = s.zwt + m.div(rsub_top * dt, 1000.0f, r1000) / rous;
+    h2o[L] = h2o[L] + MAXF(0.0f, (s.wa - 5000.0f));
+    s.wa = MINF(s.wa, 5000.0f);
+  } else {
+    float rsub_top_tot = -rsub_top * dt;
+    if (rsub_top_tot > zero) { errval = rsub_top_tot; return 3; }
+    bool active = true;
+#pragma unroll
+    for (int i = 1; i <= L; i++) {
+      if (active && i >= jwt2 + 1) {
+        const float s_y = sy[i];
+        float rstl = MAXF(rsub_top_tot, -(s_y * (g.zi(i) - zwtmm)));
+        rstl = MINF(rstl, zero);
+        h2o[i] = h2o[i] + rstl;
+        rsub_top_tot = rsub_top_tot - rstl;
+        if (rsub_top_tot >= zero) {
+          s.zwt = s.zwt - m.div(rstl / s_y, 1000.0f, r1000);
+          active = false;
+        } else {
+          s.zwt = g.zi(i) / 1000.0f;
+        }
+      }
+    }
+    s.zwt = s.zwt - m.div(rsub_top_tot, 1000.0f, r1000) / rous;
+    s.wa = s.wa + rsub_top_tot;
+    jwt3 = jwt_of<L>(s.zwt, zim);
+  }
+  // :1122-1123
+  s.zwt = MAXF(0.0f, s.zwt);
+  s.zwt = MINF(80.0f, s.zwt);
+  cs.launder();
+  // :1131-1137 saturation excess, bottom-up bucket
+#pragma unroll
+  for (int i = L; i >= 2; i--) {
+    const float cap = MAXF(0.01f, TS(i)) * g.dz(i);
+    const float xsi = MAXF(h2o[i] - cap, zero);
+    h2o[i] = MINF(cap, h2o[i]);
+    h2o[i - 1] = h2o[i - 1] + xsi;
+  }
+  // :1144-1152
+  const float xs1 = MAXF(MAXF(h2o[1], zero) - cs.sc(PS_TSDZ1), zero);
+  h2o[1] = MINF(cs.sc(PS_TSDZ1), h2o[1]);
+  const float qflx_rsub_sat = m.div(xs1, dt, g.rdt());
+  // :1161-1174 watmin top-down
+#pragma unroll
+  for (int i = 1; i <= L - 1; i++) {
+    float xs = zero;
+    if (h2o[i] < watmin) {
+      xs = watmin - h2o[i];
+      if (i == jwt3) s.zwt = s.zwt + m.div(xs / MAXF(0.01f, TS(i)), 1000.0f, r1000);
+    }
+    h2o[i] = h2o[i] + xs;
+    h2o[i + 1] = h2o[i + 1] - xs;
+  }
+  // :1180-1211 bottom layer from above
+  float xs = zero;
+  if (h2o[L] < watmin) {
+    xs = watmin - h2o[L];
+    bool active = true;
+#pragma unroll
+    for (int j = L - 1; j >= 1; j--) {
+      if (active) {
+        const float avail = MAXF(h2o[j] - watmin - xs, zero);
+        if (avail >= xs) {
+          h2o[L] = h2o[L] + xs;
+          h2o[j] = h2o[j] - xs;
+          xs = zero;
+          active = false;
+        } else {
+          h2o[L] = h2o[L] + avail;
+          h2o[j] = h2o[j] - avail;
+          xs = xs - avail;
+        }
+      }
+    }
+  }
+  h2o[L] = h2o[L] + xs;
+  rsub_top = rsub_top - m.div(xs, dt, g.rdt());
+  // :1221-1236
+  float w1 = ((1.0f - frac_h2osfc) * (qflx_surf + evg + tran) + rsub_top + qflx_rsub_sat) * dt + s.wa;
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    w1 = w1 + h2o[i];
+    theta[i] = m.div(MAXF(h2o[i], 1.0E-6f), g.thk(i), g.rthk(i));
+  }
+  // :1244
+  if (absf(w1 - w0) > 0.1f) { errval = w1 - w0; return 4; }
+  // :1282-1283
+  rnf_sum = rnf_sum + qflx_surf * dt;
+  rnf_sum = rnf_sum + rsub_top * dt;
+  return 0;
+#undef TS
+#undef HKS
+#undef BSW
+#undef PSI
+#undef LAYF
+#undef ROOT
+#undef DC
+#undef OWN
+}
+
+// Exact re-run of a substep from the rollback area (rare path, out of line):
+// one lane computes every layer with the full glibc special-case logic.
+template <int L, class G, class CS>
+H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const double *l2) {
+  St<L> s;
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    s.h2o[i] = cs.lay(PF_SVH2O, i);
+    s.smp[i] = cs.lay(PF_SVSMP, i);
+  }
+  s.zwt = cs.sc(PS_SVZWT);
+  s.wa = cs.sc(PS_SVWA);
+  float rnf = cs.sc(PS_SVRNF), errval = zero;
+  float theta[L + 1];
+  MathExact me{{e2, l2}};
+  const SplitAll sa;
+  const int code = hydrology_pair<L, G, MathExact, SplitAll, CS>(*g, cs, sa, s, theta, rnf, errval, me);
+  cs.launder();
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    cs.set_lay(PF_SVH2O, i, s.h2o[i]);
+    cs.set_lay(PF_SVSMP, i, s.smp[i]);
+  }
+  cs.set_sc(PS_SVZWT, s.zwt);
+  cs.set_sc(PS_SVWA, s.wa);
+  cs.set_sc(PS_SVRNF, rnf);
+  cs.set_sc(PS_SVERR, errval);
+  return code;
+}
+
+// One substep, speculate-then-verify (as substep in h9g_step.h).  A pair
+// re-runs if either of its lanes saw a special-path input.
+template <int L, class G, class SP, class CS>
+H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta, float &rnf_sum,
+                        float &errval, const h9m::Tabs &T) {
+  save_layers<L>(sp, cs, PF_SVH2O, s.h2o);
+  save_layers<L>(sp, cs, PF_SVSMP, s.smp);
+  cs.set_sc(PS_SVZWT, s.zwt);
+  cs.set_sc(PS_SVWA, s.wa);
+  cs.set_sc(PS_SVRNF, rnf_sum);
+  MathFast mf{T, false};
+  int code = hydrology_pair<L, G, MathFast, SP, CS>(g, cs, sp, s, theta, rnf_sum, errval, mf);
+  if (__builtin_expect(sp.pair_any(mf.special), 0)) {
+    cs.launder();
+    code = substep_exact_pair<L, G, CS>(&g, cs, T.exp2, T.log2);
+    cs.launder();
+#pragma unroll
+    for (int i = 1; i <= L; i++) {
+      s.h2o[i] = cs.lay(PF_SVH2O, i);
+      s.smp[i] = cs.lay(PF_SVSMP, i);
+      theta[i] = MAXF(s.h2o[i], 1.0E-6f) / g.thk(i);     // HYDROLOGY.f90:1233
+    }
+    s.zwt = cs.sc(PS_SVZWT);
+    s.wa = cs.sc(PS_SVWA);
+    rnf_sum = cs.sc(PS_SVRNF);
+    errval = cs.sc(PS_SVERR);
+  }
+  return code;
+}
+
+// One calendar year for one cell (HYBRID9.f90:150-290), as cell_year.
+template <int L, class G, class SP, class CS>
+H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float *forc, size_t fday,
+                          size_t fvar, int nt, int nisurf, int grow_on, float *acc, size_t astride,
+                          int &eday, int &estep, float &errval, const h9m::Tabs &T) {
+  enum { A_NPP = 0, A_PM, A_RNF, A_EVAP, A_TAS, A_RLDS, A_RSDS, A_HUSS, A_PS, A_PR, A_RHS,
+         A_THETA, A_H2O = 11 + L };
+  float *A = acc;
+  const size_t as = astride;
+  float rnf_sum = zero;
+  float theta[L + 1];
+#pragma unroll
+  for (int i = 1; i <= L; i++) theta[i] = zero;
+#pragma unroll
+  for (int k = 0; k < 12 + L; k++) A[k * as] = zero;
+  float npp = zero;
+  int code = 0;
+  MathExact me{T};
+  for (int day = 0; day < nt; day++) {
+    cs.launder();
+    opaque(A);
+    const float *f = forc + (size_t)day * fday;
+    opaque(f);
+    {
+      const Day d = make_day(f[0 * fvar], f[1 * fvar], f[2 * fvar], f[3 * fvar], f[4 * fvar],
+                             f[5 * fvar], f[6 * fvar]);                // :168-184
+      day_consts(d, s.LAI, s.LAI_litter, cs, me);
+    }
+    for (int ns = 0; ns < nisurf; ns++) {                            // :193-211
+      code = substep_pair<L, G, SP, CS>(g, cs, sp, s, theta, rnf_sum, errval, T);
+      if (code) { eday = day; estep = ns; break; }
+    }
+    if (code) return code;
+    cs.launder();
+    opaque(A);
+    opaque(f);                 // re-read the day's forcing (not kept live over the substeps)
+    const float tas = f[0 * fvar], rlds = f[1 * fvar], rsds = f[2 * fvar], huss = f[3 * fvar];
+    const float ps = f[4 * fvar], pr = f[5 * fvar], rhs = f[6 * fvar];
+    if (grow_on) grow_day<L, G, MathExact>(g, tas, s, cs, npp, me);  // :217
+    A[A_TAS * as] = A[A_TAS * as] + tas;                              // :235-254
+    A[A_RLDS * as] = A[A_RLDS * as] + rlds;
+    A[A_RSDS * as] = A[A_RSDS * as] + rsds;
+    A[A_HUSS * as] = A[A_HUSS * as] + huss;
+    A[A_PS * as] = A[A_PS * as] + ps;
+    A[A_PR * as] = A[A_PR * as] + pr;
+    A[A_RHS * as] = A[A_RHS * as] + rhs;
+    A[A_PM * as] = A[A_PM * as] + s.pm;
+    A[A_NPP * as] = A[A_NPP * as] + npp;
+    float h2o_sum = A[A_H2O * as];
+#pragma unroll
+    for (int i = 1; i <= L; i++) {
+      A[(A_THETA + i - 1) * as] = A[(A_THETA + i - 1) * as] + theta[i];
+      h2o_sum = h2o_sum + s.h2o[i];
+    }
+    A[A_H2O * as] = h2o_sum;
+  }
+  // :263-290
+  opaque(A);
+  A[A_PM * as] = A[A_PM * as] / (float)nt;
+  A[A_RNF * as] = rnf_sum / (float)(nt * nisurf);
+  A[A_EVAP * as] = zero / (float)(nt * nisurf);
+#pragma unroll
+  for (int k = A_TAS; k <= A_H2O; k++) A[k * as] = A[k * as] / (float)nt;
+  return 0;
+}
+
+}  // namespace h9k

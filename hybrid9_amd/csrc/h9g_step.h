@@ -179,6 +179,10 @@ struct CellStore {
   __device__ __forceinline__ float get(int f) const { return b[f * 64]; }
   __device__ __forceinline__ void set(int f, float x) const { b[f * 64] = x; }
   __device__ __forceinline__ void launder() { asm volatile("" : "+v"(b)); }
+  __device__ __forceinline__ float day(int f) const { return get(Lay<L>::DAY + f); }
+  __device__ __forceinline__ void set_day(int f, float x) const { set(Lay<L>::DAY + f, x); }
+  __device__ __forceinline__ float root(int i) const { return get(Lay<L>::ROOTR + i - 1); }
+  __device__ __forceinline__ void set_root(int i, float x) const { set(Lay<L>::ROOTR + i - 1, x); }
 };
 #else
 typedef float lds_float;
@@ -188,6 +192,10 @@ struct CellStore {
   inline float get(int f) const { return b[f]; }
   inline void set(int f, float x) const { b[f] = x; }
   inline void launder() {}
+  inline float day(int f) const { return get(Lay<L>::DAY + f); }
+  inline void set_day(int f, float x) const { set(Lay<L>::DAY + f, x); }
+  inline float root(int i) const { return get(Lay<L>::ROOTR + i - 1); }
+  inline void set_root(int i, float x) const { set(Lay<L>::ROOTR + i - 1, x); }
 };
 #endif
 
@@ -234,13 +242,13 @@ H9K_HD int jwt_of(float zwt, const float *zim) {
   return jwt;
 }
 
-// Day constants into the store.  M = MathExact (once per cell-day).
-template <int L, class M>
-H9K_HD void day_consts(const Day &d, float LAI, float LAI_litter, const CellStore<L> &cs, M &m) {
-  const int D = Lay<L>::DAY;
+// Day constants into the store (any store type with set_day).  M = MathExact
+// (once per cell-day).
+template <class CS, class M>
+H9K_HD void day_consts(const Day &d, float LAI, float LAI_litter, const CS &cs, M &m) {
   const float tak = d.tak;
-  cs.set(D + D_FORC, d.forc_rain);
-  cs.set(D + D_OK, ((LAI > zero) && (d.PAR > zero)) ? one : zero);
+  cs.set_day(D_FORC, d.forc_rain);
+  cs.set_day(D_OK, ((LAI > zero) && (d.PAR > zero)) ? one : zero);
   const float tsv = tak * (one + d.huss * deltx);                       // :232
   const float rho = d.ps / (rgas * tsv);                                // :236
   const float tc = tak - tf + 237.3f;
@@ -251,14 +259,14 @@ H9K_HD void day_consts(const Day &d, float LAI, float LAI_litter, const CellStor
   esat = esat * 18.0f / (gasc * tak);                                   // :255
   const float VDD = esat * (one - d.rh / 100.0f);                       // :259
   const float gamma = (cp * d.ps / (d.lamb * 0.622f)) * (18.0E-3f / (gasc * tak));  // :263
-  cs.set(D + D_DESAT, desatdT);
-  cs.set(D + D_GAMMA, gamma);
-  cs.set(D + D_VDD, VDD);
+  cs.set_day(D_DESAT, desatdT);
+  cs.set_day(D_GAMMA, gamma);
+  cs.set_day(D_VDD, VDD);
   // :283-295 (beta enters per substep)
-  cs.set(D + D_X, (1.0f / (d.PAR / (d.PAR + 300.0f))) * 400.0f);
-  cs.set(D + D_LAI2, 2.0f * LAI);
-  cs.set(D + D_PW28, m.powf(2.8f, -80.0f * MAXF(zero, VDD) / rho));
-  cs.set(D + D_RSCMIN, 1.0f / ((LAI / 2.7f) * 0.9f / (rho * 1.0E3f / 18.0f)));
+  cs.set_day(D_X, (1.0f / (d.PAR / (d.PAR + 300.0f))) * 400.0f);
+  cs.set_day(D_LAI2, 2.0f * LAI);
+  cs.set_day(D_PW28, m.powf(2.8f, -80.0f * MAXF(zero, VDD) / rho));
+  cs.set_day(D_RSCMIN, 1.0f / ((LAI / 2.7f) * 0.9f / (rho * 1.0E3f / 18.0f)));
   // :302-318
   const float rac = (LAI > zero) ? 25.0f / (2.0f * LAI) : 1.0E6f;
   float raa, ras;
@@ -269,12 +277,12 @@ H9K_HD void day_consts(const Day &d, float LAI, float LAI_litter, const CellStor
     raa = 42.0f;
     ras = 128.0f;
   }
-  cs.set(D + D_RAC, rac);
-  cs.set(D + D_RAA, raa);
-  cs.set(D + D_RAS, ras);
+  cs.set_day(D_RAC, rac);
+  cs.set_day(D_RAA, raa);
+  cs.set_day(D_RAS, ras);
   // :326-330 litter factors
-  cs.set(D + D_LIT, 10.0f + 1000.0f * LAI_litter);
-  cs.set(D + D_LIT1000, 1000.0f * LAI_litter);
+  cs.set_day(D_LIT, 10.0f + 1000.0f * LAI_litter);
+  cs.set_day(D_LIT1000, 1000.0f * LAI_litter);
   // :335-389
   const float Rnet = d.Rnet;
   const float Rnets = Rnet * m.expf(-0.7f * LAI);
@@ -284,19 +292,19 @@ H9K_HD void day_consts(const Day &d, float LAI, float LAI_litter, const CellStor
   const float rcv = rhocp * VDD;
   const float raarac = raa + rac, raaras = raa + ras;
   const float dg = desatdT + gamma;
-  cs.set(D + D_RHOCP, rhocp);
-  cs.set(D + D_A1, A1);
-  cs.set(D + D_RAARAC, raarac);
-  cs.set(D + D_RAARAS, raaras);
-  cs.set(D + D_NUMC, A1 + (rcv - desatdT * rac * (Rnets - G)) / raarac);
-  cs.set(D + D_NUMS, A1 + (rcv - desatdT * ras * (Rnet - Rnets)) / raaras);
-  cs.set(D + D_DG, dg);
-  cs.set(D + D_RA, dg * raa);
-  cs.set(D + D_DGRAS, dg * ras);
-  cs.set(D + D_DGRAC, dg * rac);
-  cs.set(D + D_DRR, desatdT * (Rnet - Rnets));
-  cs.set(D + D_DRG, desatdT * (Rnets - G));
-  cs.set(D + D_RL, rhow * d.lamb);
+  cs.set_day(D_RHOCP, rhocp);
+  cs.set_day(D_A1, A1);
+  cs.set_day(D_RAARAC, raarac);
+  cs.set_day(D_RAARAS, raaras);
+  cs.set_day(D_NUMC, A1 + (rcv - desatdT * rac * (Rnets - G)) / raarac);
+  cs.set_day(D_NUMS, A1 + (rcv - desatdT * ras * (Rnet - Rnets)) / raaras);
+  cs.set_day(D_DG, dg);
+  cs.set_day(D_RA, dg * raa);
+  cs.set_day(D_DGRAS, dg * ras);
+  cs.set_day(D_DGRAC, dg * rac);
+  cs.set_day(D_DRR, desatdT * (Rnet - Rnets));
+  cs.set_day(D_DRG, desatdT * (Rnets - G));
+  cs.set_day(D_RL, rhow * d.lamb);
 }
 
 // One HYDROLOGY call.  Returns 0 or an H9G_ERR_* code.  theta (1..L)
@@ -754,16 +762,15 @@ H9K_HD int hydrology_step(const G &g, CellStore<L> cs, St<L> &s, float *theta, f
 
 // GROW.f90:55-201 (nplants = 1, iGPT = 1).  rootr(L+1) is zeroed by the
 // caller's state write-back.
-template <int L, class G, class M>
-H9K_HD void grow_day(const G &g, float tas, St<L> &s, const CellStore<L> &cs, float &npp, M &m) {
-  typedef Lay<L> Y;
+template <int L, class G, class M, class CS>
+H9K_HD void grow_day(const G &g, float tas, St<L> &s, const CS &cs, float &npp, M &m) {
   float w_i = zero;
 #pragma unroll
   for (int i = 1; i <= L; i++) {
     float w = (-150000.0f - s.smp[i]) / (-150000.0f - (-50000.0f));
     w = MAXF(zero, w);
     w = MINF(one, w);
-    w_i = w_i + cs.get(Y::ROOTR + i - 1) * w;
+    w_i = w_i + cs.root(i) * w;
   }
   float fT;
   if ((tas - tf) > 18.0f) {
@@ -796,7 +803,7 @@ H9K_HD void grow_day(const G &g, float tas, St<L> &s, const CellStore<L> &cs, fl
 #pragma unroll
   for (int i = 1; i <= L; i++) {
     const float pw = m.powf(decay, g.zi(i) / 10.0f);
-    cs.set(Y::ROOTR + i - 1, zero + (1.0f - pw) - (1.0f - pw_prev));
+    cs.set_root(i, zero + (1.0f - pw) - (1.0f - pw_prev));
     pw_prev = pw;
   }
   npp = zero + dplant_mass;
@@ -941,7 +948,7 @@ H9K_HD int cell_year(const G &g, CellStore<L> cs, St<L> &s, const float *forc, s
     const float tas = f[0 * fvar], rlds = f[1 * fvar], rsds = f[2 * fvar], huss = f[3 * fvar];
     const float ps = f[4 * fvar], pr = f[5 * fvar], rhs = f[6 * fvar];
     const Day d = make_day(tas, rlds, rsds, huss, ps, pr, rhs);     // :168-184
-    day_consts<L>(d, s.LAI, s.LAI_litter, cs, me);
+    day_consts(d, s.LAI, s.LAI_litter, cs, me);
     for (int ns = 0; ns < nisurf; ns++) {                            // :193-211
       code = substep<L, G>(g, cs, s, theta, rnf_sum, errval, T);
       if (code) { eday = day; estep = ns; break; }

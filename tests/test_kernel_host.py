@@ -50,7 +50,9 @@ def host_run(*, zi, params, forcing, nisurf, year0, nyears, grow_on, state0, con
     return dict(rc=rc, annual=ann, state=st, err=err.reshape(n, 4))
 
 
-@pytest.mark.parametrize("const_geo", [1, 0])
+# const_geo: 1/0 = one-lane kernel body with compile-time/runtime geometry;
+# 2/3 = the pair-lane code path (h9g_pair.h, one lane doing every layer).
+@pytest.mark.parametrize("const_geo", [1, 0, 2, 3])
 @pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit")))
 def test_kernel_body_matches_reference_golden(name, const_geo):
     meta, inp, exp = load_golden(name)
@@ -60,17 +62,19 @@ def test_kernel_body_matches_reference_golden(name, const_geo):
     assert same_bits(out["state"], exp["state"])
 
 
-def test_kernel_body_reproduces_reference_stop():
+@pytest.mark.parametrize("const_geo", [1, 2])
+def test_kernel_body_reproduces_reference_stop(const_geo):
     meta, inp, _ = load_golden("stop_ns24")
-    out = host_run(const_geo=1, **inp)
+    out = host_run(const_geo=const_geo, **inp)
     s = meta["stop"]
     assert out["rc"] == s["code"]
     c = s["cell"]
     assert out["err"][c, 0] == s["code"] and out["err"][c, 2] == s["day"]
 
 
+@pytest.mark.parametrize("pair", [False, True])
 @pytest.mark.parametrize("L,nisurf,grow", [(8, 48, 0), (8, 24, 1), (10, 24, 1), (10, 48, 0)])
-def test_kernel_body_matches_oracle_random_cells(L, nisurf, grow):
+def test_kernel_body_matches_oracle_random_cells(L, nisurf, grow, pair):
     if L == 8:
         g = synth.land_cells()[7::389][:160]
         lat, zi = synth.cell_lat(g), synth.ZI_L8
