@@ -14,12 +14,15 @@ GPU, every entry point raises.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "lib" / "libh9g.so"
+if os.environ.get("H9G_LIB"):          # alternative build (e.g. the H9G_STAMPS profiling build)
+    LIB_PATH = Path(os.environ["H9G_LIB"]).resolve()
 NFORCING = 7
 NANNUAL_SCALARS = 11
 NDIAG = 12

@@ -64,6 +64,7 @@ struct KArgs {
   float *__restrict__ annual;      // (12+L) rows x ncell
   int *__restrict__ err;           // 4 rows x ncell: code, day, substep, value bits
   int *__restrict__ err_flag;
+  unsigned *__restrict__ stamps;   // H9G_STAMPS builds: 8 phase cycle sums per wave
 };
 
 __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
@@ -164,6 +165,8 @@ h9g_pair_kernel(const KArgs a, const G g) {
   __shared__ uint64_t s_e2[32];
   __shared__ double s_l2[32];
   __shared__ float s_cell[H9G_PWAVES][PS::ROWS * H9G_PLANES];   // [wave][row][lane]
+  __shared__ float s_zt[2 * (L + 2)];
+  if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -173,7 +176,7 @@ h9g_pair_kernel(const KArgs a, const G g) {
   if (c >= a.ncell) return;          // both lanes of a pair leave together
   const int n = a.ncell;
 
-  PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1]};
+  PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1], (const lds_float *)s_zt};
   const Split2 sp{h};
   St<L> s;
 #pragma unroll
@@ -212,8 +215,16 @@ h9g_pair_kernel(const KArgs a, const G g) {
   cell_inv_pair<L, G>(g, cs);
   int eday = 0, estep = 0;
   float errval = 0.0f;
+#if defined(H9G_STAMPS)
+  StampProf pr{stamp_clock(), {0, 0, 0, 0, 0, 0, 0, 0}};
+  const int code = cell_year_pair<L, G>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar, a.nt, a.nisurf,
+                                        a.grow_on, a.annual + c, (size_t)n, eday, estep, errval, T, pr);
+  if (lane == 0 && a.stamps)
+    for (int k = 0; k < 8; k++) a.stamps[(blockIdx.x * H9G_PWAVES + wave) * 8 + k] = pr.acc[k];
+#else
   const int code = cell_year_pair<L, G>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar, a.nt, a.nisurf,
                                         a.grow_on, a.annual + c, (size_t)n, eday, estep, errval, T);
+#endif
   if (h != 0) return;                // the even lane writes the cell back
   int cw = c;
   opaque(cw);
@@ -226,6 +237,90 @@ h9g_pair_kernel(const KArgs a, const G g) {
     if (a.grow_on) a.st[(size_t)(3 * L + i - 1) * n + cw] = cs.lay(PF_ROOTR, i);
   }
   if (a.grow_on) a.st[(size_t)(4 * L) * n + cw] = zero;   // rootr_col(Nlevgrnd)
+  a.st[ow + 0 * (size_t)n] = s.zwt;
+  a.st[ow + 1 * (size_t)n] = s.wa;
+  a.st[ow + 2 * (size_t)n] = s.LAI;
+  a.st[ow + 3 * (size_t)n] = s.LAI_litter;
+  a.st[ow + 4 * (size_t)n] = s.pm;
+  a.st[ow + 5 * (size_t)n] = s.pfm;
+  a.st[ow + 6 * (size_t)n] = s.plen;
+  a.st[ow + 7 * (size_t)n] = s.rdepth;
+  if (code) {
+    a.err[0 * (size_t)n + cw] = code;
+    a.err[1 * (size_t)n + cw] = eday;
+    a.err[2 * (size_t)n + cw] = estep;
+    a.err[3 * (size_t)n + cw] = __builtin_bit_cast(int, errval);
+    atomicOr(a.err_flag, 1);
+#pragma unroll
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + cw] = __builtin_nanf("");
+  }
+}
+
+// Solo kernel: one lane per soil column running the generic code of
+// h9g_pair.h with one lane doing every layer (SplitAll: two layers per
+// scheduling region, tridiagonal rows eliminated as assembled).
+template <int L, class G>
+__global__ void __launch_bounds__(H9G_YBLOCK) __attribute__((amdgpu_waves_per_eu(2, 2)))
+h9g_solo_kernel(const KArgs a, const G g) {
+  typedef SoloStore<L> SS;
+  __shared__ uint64_t s_e2[32];
+  __shared__ double s_l2[32];
+  __shared__ float s_cell[SS::ROWS * H9G_YBLOCK];
+  __shared__ float s_zt[2 * (L + 2)];
+  if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
+  load_tabs(s_e2, s_l2);
+  const h9m::Tabs T = {s_e2, s_l2};
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.ncell) return;
+  const int n = a.ncell;
+  SS cs{(lds_float *)&s_cell[threadIdx.x], (const lds_float *)s_zt};
+  const SplitAll sp;
+  St<L> s;
+#pragma unroll
+  for (int p = 0; p < 4; p++)
+#pragma unroll
+    for (int i = 1; i <= L; i++) cs.set_lay(p, i, a.par[(size_t)(p * L + i - 1) * n + c]);
+  cs.set_sc(PS_FMAX, a.par[(size_t)(4 * L) * n + c]);
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    s.h2o[i] = a.st[(size_t)(0 * L + i - 1) * n + c];
+    s.smp[i] = a.st[(size_t)(2 * L + i - 1) * n + c];
+    cs.set_lay(PF_ROOTR, i, a.st[(size_t)(3 * L + i - 1) * n + c]);
+  }
+  const size_t o8 = (size_t)(4 * L + 1) * n + c;
+  s.zwt = a.st[o8 + 0 * (size_t)n];
+  s.wa = a.st[o8 + 1 * (size_t)n];
+  s.LAI = a.st[o8 + 2 * (size_t)n];
+  s.LAI_litter = a.st[o8 + 3 * (size_t)n];
+  s.pm = a.st[o8 + 4 * (size_t)n];
+  s.pfm = a.st[o8 + 5 * (size_t)n];
+  s.plen = a.st[o8 + 6 * (size_t)n];
+  s.rdepth = a.st[o8 + 7 * (size_t)n];
+  cs.launder();
+  float ts_sum = zero;
+#pragma unroll
+  for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.lay(PF_TS, i);
+  if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
+#pragma unroll
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + c] = __builtin_nanf("");
+    return;
+  }
+  cell_inv_pair<L, G>(g, cs);
+  int eday = 0, estep = 0;
+  float errval = 0.0f;
+  const int code = cell_year_pair<L, G>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar, a.nt, a.nisurf,
+                                        a.grow_on, a.annual + c, (size_t)n, eday, estep, errval, T);
+  int cw = c;
+  opaque(cw);
+  cs.launder();
+  const size_t ow = (size_t)(4 * L + 1) * n + cw;
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    a.st[(size_t)(0 * L + i - 1) * n + cw] = s.h2o[i];
+    a.st[(size_t)(2 * L + i - 1) * n + cw] = s.smp[i];
+    if (a.grow_on) a.st[(size_t)(3 * L + i - 1) * n + cw] = cs.lay(PF_ROOTR, i);
+  }
+  if (a.grow_on) a.st[(size_t)(4 * L) * n + cw] = zero;
   a.st[ow + 0 * (size_t)n] = s.zwt;
   a.st[ow + 1 * (size_t)n] = s.wa;
   a.st[ow + 2 * (size_t)n] = s.LAI;
@@ -392,7 +487,9 @@ struct h9g_ctx {
   int params_set = 0, state_set = 0, ran = 0;
   h9g_error last_err{};
   const char *kname = "";
-  int pair = 1;        // 1: h9g_pair_kernel (default), 0: h9g_year_kernel (H9G_KERNEL=single)
+  unsigned *d_stamps = nullptr;   // H9G_STAMPS builds only
+  int kind = 1;        // 1: h9g_pair_kernel (default), 0: h9g_year_kernel (H9G_KERNEL=single),
+                       // 2: h9g_solo_kernel (H9G_KERNEL=solo)
 };
 
 #define HIPCHK(x)                                                              \
@@ -476,6 +573,7 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_diag);
   (void)hipFree(ctx->d_gid);
   (void)hipFree(ctx->d_lat);
+  (void)hipFree(ctx->d_stamps);
   for (auto e : ctx->ev_copied) hipEventDestroy(e);
   for (auto e : ctx->ev_consumed) hipEventDestroy(e);
   for (int i = 0; i < NEVT; i++) {
@@ -531,15 +629,19 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     h9g_destroy(ctx);
     return nullptr;
   }
-  static const char *names[2][2][3] = {
+  static const char *names[3][2][3] = {
       {{"h9g_year_kernel<8,GeoR>", "h9g_year_kernel<8,GeoC<8,24>>", "h9g_year_kernel<8,GeoC<8,48>>"},
        {"h9g_year_kernel<10,GeoR>", "h9g_year_kernel<10,GeoC<10,24>>", "h9g_year_kernel<10,GeoC<10,48>>"}},
       {{"h9g_pair_kernel<8,GeoR>", "h9g_pair_kernel<8,GeoC<8,24>>", "h9g_pair_kernel<8,GeoC<8,48>>"},
-       {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}}};
+       {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}},
+      {{"h9g_solo_kernel<8,GeoR>", "h9g_solo_kernel<8,GeoC<8,24>>", "h9g_solo_kernel<8,GeoC<8,48>>"},
+       {"h9g_solo_kernel<10,GeoR>", "h9g_solo_kernel<10,GeoC<10,24>>", "h9g_solo_kernel<10,GeoC<10,48>>"}}};
   const char *kenv = getenv("H9G_KERNEL");
-  ctx->pair = !(kenv && strcmp(kenv, "single") == 0);
+  ctx->kind = 1;
+  if (kenv && strcmp(kenv, "single") == 0) ctx->kind = 0;
+  if (kenv && strcmp(kenv, "solo") == 0) ctx->kind = 2;
   const GeoKind gk = geo_kind(*cfg);
-  ctx->kname = names[ctx->pair][L == 8 ? 0 : 1][gk == GEO_R ? 0 : (gk == GEO_C24 ? 1 : 2)];
+  ctx->kname = names[ctx->kind][L == 8 ? 0 : 1][gk == GEO_R ? 0 : (gk == GEO_C24 ? 1 : 2)];
   return ctx;
 }
 
@@ -683,6 +785,12 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   a.annual = ctx->d_ann;
   a.err = ctx->d_err;
   a.err_flag = ctx->d_errflag;
+  a.stamps = nullptr;
+#if defined(H9G_STAMPS)
+  if (!ctx->d_stamps) HIPCHK(hipMalloc(&ctx->d_stamps, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8)));
+  HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8), ctx->sc));
+  a.stamps = ctx->d_stamps;
+#endif
   if (ctx->nev >= NEVT) {   // fold finished timings before reusing events
     HIPCHK(hipStreamSynchronize(ctx->sc));
     for (int i = 0; i < ctx->nev; i++) {
@@ -695,7 +803,10 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   }
   const int e = ctx->nev++;
   HIPCHK(hipEventRecord(ctx->ev0[e], ctx->sc));
-  if (ctx->pair) {
+  if (ctx->kind == 2) {
+    H9G_DISPATCH(ctx, h9g_solo_kernel, (unsigned)((ctx->n + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
+                 ctx->sc, a);
+  } else if (ctx->kind == 1) {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n + per_block - 1) / per_block), 64 * H9G_PWAVES,
                  ctx->sc, a);
@@ -725,6 +836,20 @@ int h9g_sync(h9g_ctx *ctx) {
     ctx->last_ms = ms;
   }
   ctx->nev = 0;
+#if defined(H9G_STAMPS)
+  if (ctx->d_stamps && ctx->kind == 1) {   // mean shader cycles per wave and substep, by phase
+    const size_t nw = (ctx->n + H9G_PCPW - 1) / H9G_PCPW;
+    std::vector<unsigned> st(8 * nw);
+    HIPCHK(hipMemcpy(st.data(), ctx->d_stamps, sizeof(unsigned) * 8 * nw, hipMemcpyDeviceToHost));
+    double sum[8] = {0}, tot = 0;
+    for (size_t w = 0; w < nw; w++)
+      for (int k = 0; k < 8; k++) sum[k] += st[8 * w + k];
+    const double steps = (double)nw * days_in_year(ctx->last_year) * ctx->cfg.nisurf;
+    fprintf(stderr, "h9g stamps (cycles/wave/substep):");
+    for (int k = 0; k < 8; k++) { fprintf(stderr, " p%d=%.0f", k, sum[k] / steps); tot += sum[k]; }
+    fprintf(stderr, " total=%.0f\n", tot / steps);
+  }
+#endif
   int flag = 0;
   HIPCHK(hipMemcpy(&flag, ctx->d_errflag, sizeof(int), hipMemcpyDeviceToHost));
   if (!flag) return 0;

@@ -75,6 +75,9 @@ template <int L>
 struct FlatStore {                     // host: one flat array per cell
   static constexpr int N = PF_N * L + PS_N;
   float *b;
+  const float *zt;                     // zi(0..L+1), then zi(0..L+1)/1000
+  H9K_HD float zi(int i) const { return zt[i]; }
+  H9K_HD float zim(int i) const { return zt[L + 2 + i]; }
   H9K_HD float lay(int p, int i) const { return b[p * L + i - 1]; }
   H9K_HD void set_lay(int p, int i, float v) const { b[p * L + i - 1] = v; }
   H9K_HD float sc(int k) const { return b[PF_N * L + k]; }
@@ -99,6 +102,9 @@ struct PairStore {
   static constexpr int NT = L / 2;
   static constexpr int ROWS = PF_N * NT + (PS_N + 1) / 2;
   lds_float *self, *even;
+  const lds_float *zt;                 // zi(0..L+1), then zi(0..L+1)/1000 (per block)
+  __device__ __forceinline__ float zi(int i) const { return zt[i]; }
+  __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
   __device__ __forceinline__ float lay(int p, int i) const {
     return even[(p * NT + ((i - 1) >> 1)) * S + ((i - 1) & 1)];
   }
@@ -113,7 +119,7 @@ struct PairStore {
   __device__ __forceinline__ void set_slot(int p, int t, float v) const { self[(p * NT + t) * S] = v; }
   __device__ __forceinline__ void launder() {
 #if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+v"(self), "+v"(even)::"memory");
+    asm volatile("" : "+v"(self), "+v"(even), "+v"(zt)::"memory");
 #endif
   }
   __device__ __forceinline__ float day(int f) const { return sc(PS_DAY + f); }
@@ -121,6 +127,55 @@ struct PairStore {
   __device__ __forceinline__ float root(int i) const { return lay(PF_ROOTR, i); }
   __device__ __forceinline__ void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
 };
+
+// Device, one lane per column ("solo"): column `lane` of a [row][64] block,
+// every field in the lane's own column.
+template <int L>
+struct SoloStore {
+  static constexpr int ROWS = PF_N * L + PS_N;
+  lds_float *b;
+  const lds_float *zt;
+  __device__ __forceinline__ float zi(int i) const { return zt[i]; }
+  __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
+  __device__ __forceinline__ float lay(int p, int i) const { return b[(p * L + i - 1) * 64]; }
+  __device__ __forceinline__ void set_lay(int p, int i, float v) const { b[(p * L + i - 1) * 64] = v; }
+  __device__ __forceinline__ float sc(int k) const { return b[(PF_N * L + k) * 64]; }
+  __device__ __forceinline__ void set_sc(int k, float v) const { b[(PF_N * L + k) * 64] = v; }
+  __device__ __forceinline__ float slot(int p, int t) const { return b[(p * L + 2 * t) * 64]; }
+  __device__ __forceinline__ void set_slot(int p, int t, float v) const { b[(p * L + 2 * t) * 64] = v; }
+  __device__ __forceinline__ void launder() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(b), "+v"(zt)::"memory");
+#endif
+  }
+  __device__ __forceinline__ float day(int f) const { return sc(PS_DAY + f); }
+  __device__ __forceinline__ void set_day(int f, float v) const { set_sc(PS_DAY + f, v); }
+  __device__ __forceinline__ float root(int i) const { return lay(PF_ROOTR, i); }
+  __device__ __forceinline__ void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
+};
+
+// Phase profiler (tools: H9G_STAMPS build only).  NoProf compiles away.
+struct NoProf {
+  H9K_HD void mark(int) {}
+};
+#if defined(H9G_STAMPS)
+H9K_HD uint64_t stamp_clock() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_s_memtime();
+#else
+  return 0;
+#endif
+}
+struct StampProf {                     // wave-uniform shader-clock deltas per phase
+  uint64_t last;
+  uint32_t acc[8];
+  H9K_HD void mark(int k) {
+    const uint64_t t = stamp_clock();
+    acc[k] += (uint32_t)(t - last);
+    last = t;
+  }
+};
+#endif
 
 // ---------------------------------------------------------------- policies
 // One lane computes every layer.
@@ -197,6 +252,36 @@ H9K_HD void save_layers(const Split2 &sp, const CS &cs, int p, const float *v) {
   for (int t = 0; t < L / 2; t++) cs.set_slot(p, t, sel(sp.h, v[2 * t + 1], v[2 * t + 2]));
 }
 
+// Runs visit(k) for k = 0, 1, ... while it returns true (the reference's
+// layer loops with EXIT).  The fast path (MathFast) unrolls two visits --
+// the second only if some lane needs it -- and hands a third to the exact
+// re-run; loops visit one layer 99.5% of the time and never three in the
+// synthetic runs.  MathExact loops.
+template <class M, class F>
+H9K_HD void visit_layers(M &m, F visit) {
+  if constexpr (M::kExact) {
+    for (int k = 0;; k++)
+      if (!visit(k)) break;
+  } else {
+    bool more = visit(0);
+    if (any_lane(more)) {
+      if (more) more = visit(1);
+      m.special |= more;
+    }
+  }
+}
+
+// Runtime-indexable geometry table: zi(0..L+1), then zi(0..L+1)/1000
+// (the reference's zi(I)/1000.0, e.g. HYDROLOGY.f90:499-508,998).
+template <int L, class G, class T>
+H9K_HD void fill_zt(const G &g, T *zt) {
+#pragma unroll
+  for (int i = 0; i <= L + 1; i++) {
+    zt[i] = g.zi(i);
+    zt[L + 2 + i] = g.zi(i) / 1000.0f;
+  }
+}
+
 // Parameter-only invariants (as cell_inv), into a pair/flat store.
 template <int L, class G, class CS>
 H9K_HD void cell_inv_pair(const G &g, const CS &cs) {
@@ -221,9 +306,9 @@ H9K_HD void cell_inv_pair(const G &g, const CS &cs) {
 
 // One HYDROLOGY call (HYDROLOGY.f90:141-1283), pair-split.  Same contract
 // as hydrology_step (h9g_step.h), whose comments cite each block.
-template <int L, class G, class M, class SP, class CS>
+template <int L, class G, class M, class SP, class CS, class PR = NoProf>
 H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta,
-                          float &rnf_sum, float &errval, M &m) {
+                          float &rnf_sum, float &errval, M &m, PR &pr) {
   constexpr int NT = L / 2;
   const float dt = g.dt();
   constexpr double r1000 = 1.0 / 1000.0;
@@ -309,6 +394,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
   const int jwt = jwt_of<L>(s.zwt, zim);
   const bool aq = (jwt == L);
   cs.launder();
+  pr.mark(1);
 
   // :517-567 equilibrium profile, own layers
   float zq[L + 2];
@@ -381,6 +467,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
   zq[L + 1] = aq ? eA.v[0] : zero;
   const float smp1 = eS.v[0], dsmpdw1 = eS.v[1];
   cs.launder();
+  pr.mark(2);
 
   // :598-639 conductivity and matric potential, own layers
   float hk[L + 1], dhkdw[L + 1], dsmpdw[L + 1];
@@ -411,6 +498,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
         },
         out);
   }
+  pr.mark(3);
   // :645-650 aquifer node geometry
   const float zcA = 0.5f * (zwtmm + g.zc(L));
   const float dzA = (jwt < L) ? g.dz(L) : zwtmm - g.zc(L);
@@ -493,6 +581,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
 #pragma unroll
   for (int i = 1; i <= L; i++) h2o[i] = h2o[i] + dwat2[i] * g.dz(i);
   cs.launder();
+  pr.mark(4);
   // :856-904 recharge
   float qcharge;
   if (jwt < L) {
@@ -518,20 +607,15 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
   } else {
     qcharge = m.div(dwat2[L + 1] * dzA, dt, g.rdt());
   }
-  // :923-1009 water table from recharge; specific yields s_y(I) for the
-  // current zwtmm, all layers only if some lane has its water table inside
-  // the column (sy(L) = rous came from the pair split above)
-  float sy[L + 1];
-  sy[L] = MAXF(TS(L) * (one - pY.v[0]), 0.02f);
-  if (any_lane(jwt < L)) {
-    float *const out[1] = {sy};
-    sp.template par<NT, 1>(
-        [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
-          return FV<1>{{MAXF(OWN(PF_TS) * (one - m.powf((one + zwtmm / (-OWN(PF_PSI))), OWN(PF_NINVB))), 0.02f)}};
-        },
-        out);
-  }
-  float rous = sy[L];
+  // :923-1009 water table from recharge.  The specific yield s_y(I)
+  // (:963-965, :979-981, :1077-1080) is evaluated for exactly the layers the
+  // loops visit (usually one), at a runtime layer index; rous = s_y(L) of
+  // the pre-update zwtmm came from the pair split above.
+  auto s_y_at = [&](int i, float zmm) __attribute__((always_inline)) -> float {
+    return MAXF(cs.lay(PF_TS, i) * (one - m.powf((one + zmm / (-cs.lay(PF_PSI, i))), cs.lay(PF_NINVB, i))),
+                0.02f);
+  };
+  float rous = MAXF(TS(L) * (one - pY.v[0]), 0.02f);
   int jwt2 = jwt;
   if (jwt == L) {
     s.wa = s.wa + qcharge * dt;
@@ -539,54 +623,39 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
   } else {
     float qcharge_tot = qcharge * dt;
     if (qcharge_tot > zero) {          // rising: I = jwt+1 .. 1
-      bool active = true;
-#pragma unroll
-      for (int i = L; i >= 1; i--) {
-        if (active && i <= jwt + 1) {
-          const float s_y = sy[i];
-          float qcl = MINF(qcharge_tot, s_y * (zwtmm - g.zi(i - 1)));
-          qcl = MAXF(qcl, zero);
-          if (s_y > zero) s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
-          qcharge_tot = qcharge_tot - qcl;
-          if (qcharge_tot <= zero) active = false;
-        }
-      }
+      visit_layers(m, [&](int k) __attribute__((always_inline)) -> bool {
+        const int i = jwt + 1 - k;
+        const float s_y = s_y_at(i, zwtmm);
+        float qcl = MINF(qcharge_tot, s_y * (zwtmm - cs.zi(i - 1)));
+        qcl = MAXF(qcl, zero);
+        if (s_y > zero) s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
+        qcharge_tot = qcharge_tot - qcl;
+        return !(qcharge_tot <= zero || i == 1);
+      });
     } else {                            // deepening: I = jwt+1 .. L
-      bool active = true;
-#pragma unroll
-      for (int i = 1; i <= L; i++) {
-        if (active && i >= jwt + 1) {
-          const float s_y = sy[i];
-          float qcl = MAXF(qcharge_tot, -s_y * (g.zi(i) - zwtmm));
-          qcl = MINF(qcl, zero);
-          qcharge_tot = qcharge_tot - qcl;
-          if (qcharge_tot >= zero) {
-            s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
-            active = false;
-          } else {
-            s.zwt = g.zi(i) / 1000.0f;
-          }
+      visit_layers(m, [&](int k) __attribute__((always_inline)) -> bool {
+        const int i = jwt + 1 + k;
+        const float s_y = s_y_at(i, zwtmm);
+        float qcl = MAXF(qcharge_tot, -s_y * (cs.zi(i) - zwtmm));
+        qcl = MINF(qcl, zero);
+        qcharge_tot = qcharge_tot - qcl;
+        if (qcharge_tot >= zero) {
+          s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
+          return false;
         }
-      }
+        s.zwt = cs.zim(i);
+        return i != L;
+      });
       if (qcharge_tot > zero) s.zwt = s.zwt - m.div(qcharge_tot, 1000.0f, r1000) / rous;
     }
     jwt2 = jwt_of<L>(s.zwt, zim);
   }
   cs.launder();
-  // :1015-1035 baseflow; s_y for the new zwtmm (:1077-1080)
+  pr.mark(5);
+  // :1015-1035 baseflow; s_y(L) for the new zwtmm (:1077-1080)
   zwtmm = 1000.0f * s.zwt;
   float rsub_top = 5.5E-3f * m.expf(-fff * s.zwt);
-  if (any_lane(jwt2 < L)) {
-    float *const out[1] = {sy};
-    sp.template par<NT, 1>(
-        [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
-          return FV<1>{{MAXF(OWN(PF_TS) * (one - m.powf((one + zwtmm / (-OWN(PF_PSI))), OWN(PF_NINVB))), 0.02f)}};
-        },
-        out);
-  } else {
-    sy[L] = MAXF(TS(L) * (one - m.powf((one + zwtmm / (-PSI(L))), LAYF(PF_NINVB, L))), 0.02f);
-  }
-  rous = sy[L];
+  rous = MAXF(TS(L) * (one - m.powf((one + zwtmm / (-PSI(L))), LAYF(PF_NINVB, L))), 0.02f);
   // :1048-1118
   int jwt3 = jwt2;
   if (jwt2 == L) {
@@ -597,23 +666,25 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
   } else {
     float rsub_top_tot = -rsub_top * dt;
     if (rsub_top_tot > zero) { errval = rsub_top_tot; return 3; }
-    bool active = true;
+    visit_layers(m, [&](int k) __attribute__((always_inline)) -> bool {   // I = jwt+1 .. L
+      const int i = jwt2 + 1 + k;
+      const float s_y = s_y_at(i, zwtmm);
+      float rstl = MAXF(rsub_top_tot, -(s_y * (cs.zi(i) - zwtmm)));
+      rstl = MINF(rstl, zero);
 #pragma unroll
-    for (int i = 1; i <= L; i++) {
-      if (active && i >= jwt2 + 1) {
-        const float s_y = sy[i];
-        float rstl = MAXF(rsub_top_tot, -(s_y * (g.zi(i) - zwtmm)));
-        rstl = MINF(rstl, zero);
-        h2o[i] = h2o[i] + rstl;
-        rsub_top_tot = rsub_top_tot - rstl;
-        if (rsub_top_tot >= zero) {
-          s.zwt = s.zwt - m.div(rstl / s_y, 1000.0f, r1000);
-          active = false;
-        } else {
-          s.zwt = g.zi(i) / 1000.0f;
-        }
+      for (int j = 1; j <= L; j++) {    // h2o(I) = h2o(I) + rstl, I at runtime: a select per
+        int hit = (j == i);             // layer (opaque, so it is not folded back into an
+        opaque(hit);                    // indexed store that would demote h2o to scratch)
+        h2o[j] = hit ? h2o[j] + rstl : h2o[j];
       }
-    }
+      rsub_top_tot = rsub_top_tot - rstl;
+      if (rsub_top_tot >= zero) {
+        s.zwt = s.zwt - m.div(rstl / s_y, 1000.0f, r1000);
+        return false;
+      }
+      s.zwt = cs.zim(i);
+      return i != L;
+    });
     s.zwt = s.zwt - m.div(rsub_top_tot, 1000.0f, r1000) / rous;
     s.wa = s.wa + rsub_top_tot;
     jwt3 = jwt_of<L>(s.zwt, zim);
@@ -622,6 +693,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
   s.zwt = MAXF(0.0f, s.zwt);
   s.zwt = MINF(80.0f, s.zwt);
   cs.launder();
+  pr.mark(6);
   // :1131-1137 saturation excess, bottom-up bucket
 #pragma unroll
   for (int i = L; i >= 2; i--) {
@@ -676,6 +748,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
     w1 = w1 + h2o[i];
     theta[i] = m.div(MAXF(h2o[i], 1.0E-6f), g.thk(i), g.rthk(i));
   }
+  pr.mark(7);
   // :1244
   if (absf(w1 - w0) > 0.1f) { errval = w1 - w0; return 4; }
   // :1282-1283
@@ -708,7 +781,8 @@ H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const dou
   float theta[L + 1];
   MathExact me{{e2, l2}};
   const SplitAll sa;
-  const int code = hydrology_pair<L, G, MathExact, SplitAll, CS>(*g, cs, sa, s, theta, rnf, errval, me);
+  NoProf np;
+  const int code = hydrology_pair<L, G, MathExact, SplitAll, CS>(*g, cs, sa, s, theta, rnf, errval, me, np);
   cs.launder();
 #pragma unroll
   for (int i = 1; i <= L; i++) {
@@ -724,16 +798,17 @@ H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const dou
 
 // One substep, speculate-then-verify (as substep in h9g_step.h).  A pair
 // re-runs if either of its lanes saw a special-path input.
-template <int L, class G, class SP, class CS>
+template <int L, class G, class SP, class CS, class PR>
 H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta, float &rnf_sum,
-                        float &errval, const h9m::Tabs &T) {
+                        float &errval, const h9m::Tabs &T, PR &pr) {
+  pr.mark(0);
   save_layers<L>(sp, cs, PF_SVH2O, s.h2o);
   save_layers<L>(sp, cs, PF_SVSMP, s.smp);
   cs.set_sc(PS_SVZWT, s.zwt);
   cs.set_sc(PS_SVWA, s.wa);
   cs.set_sc(PS_SVRNF, rnf_sum);
   MathFast mf{T, false};
-  int code = hydrology_pair<L, G, MathFast, SP, CS>(g, cs, sp, s, theta, rnf_sum, errval, mf);
+  int code = hydrology_pair<L, G, MathFast, SP, CS, PR>(g, cs, sp, s, theta, rnf_sum, errval, mf, pr);
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
     cs.launder();
     code = substep_exact_pair<L, G, CS>(&g, cs, T.exp2, T.log2);
@@ -753,10 +828,10 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta,
 }
 
 // One calendar year for one cell (HYBRID9.f90:150-290), as cell_year.
-template <int L, class G, class SP, class CS>
+template <int L, class G, class SP, class CS, class PR = NoProf>
 H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float *forc, size_t fday,
                           size_t fvar, int nt, int nisurf, int grow_on, float *acc, size_t astride,
-                          int &eday, int &estep, float &errval, const h9m::Tabs &T) {
+                          int &eday, int &estep, float &errval, const h9m::Tabs &T, PR &&pr = PR()) {
   enum { A_NPP = 0, A_PM, A_RNF, A_EVAP, A_TAS, A_RLDS, A_RSDS, A_HUSS, A_PS, A_PR, A_RHS,
          A_THETA, A_H2O = 11 + L };
   float *A = acc;
@@ -781,7 +856,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float
       day_consts(d, s.LAI, s.LAI_litter, cs, me);
     }
     for (int ns = 0; ns < nisurf; ns++) {                            // :193-211
-      code = substep_pair<L, G, SP, CS>(g, cs, sp, s, theta, rnf_sum, errval, T);
+      code = substep_pair<L, G, SP, CS>(g, cs, sp, s, theta, rnf_sum, errval, T, pr);
       if (code) { eday = day; estep = ns; break; }
     }
     if (code) return code;

@@ -117,12 +117,14 @@ H9K_HD double recip64(float d) {
 // 24-bit significands), and a normal-range quotient is never exactly a
 // midpoint.  Subnormal results flag the substep for the exact re-run.
 struct MathExact {
+  static constexpr bool kExact = true;
   h9m::Tabs T;
   H9K_HD float expf(float x) { return h9m::expf(x, T); }
   H9K_HD float powf(float x, float y) { return h9m::powf(x, y, T); }
   H9K_HD float div(float x, float d, double) { return x / d; }
 };
 struct MathFast {
+  static constexpr bool kExact = false;
   h9m::Tabs T;
   bool special;
   H9K_HD float expf(float x) { return h9m::expf_nx(x, T, special); }

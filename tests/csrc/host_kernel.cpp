@@ -83,8 +83,9 @@ static int run_cells_pair(const G &g, int n, int nisurf, int grow_on, int year0,
   int first = 0;
 #pragma omp parallel for schedule(dynamic, 4)
   for (int c = 0; c < n; c++) {
-    float store[FlatStore<L>::N];
-    FlatStore<L> cs{store};
+    float store[FlatStore<L>::N], zt[2 * (L + 2)];
+    fill_zt<L>(g, zt);
+    FlatStore<L> cs{store, zt};
     const SplitAll sp;
     St<L> s;
     for (int i = 1; i <= L; i++) {

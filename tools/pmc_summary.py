@@ -24,11 +24,11 @@ def counters(d: Path, kernel: str):
     return {k: sum(v) / len(v) for k, v in out.items()}, {k: len(v) for k, v in out.items()}
 
 
-def main(tag, workload="config2", kernel="h9g_year_kernel"):
+def main(tag, workload="config2", kernel="h9g_"):
     d = ROOT / "gpurun_out" / f"prof_{tag}"
-    c, n = counters(d, kernel)
     stats = list(csv.DictReader(open(d / "kt" / "kt_kernel_stats.csv")))
-    ks = [r for r in stats if kernel in r["Name"]][0]
+    ks = max((r for r in stats if kernel in r["Name"]), key=lambda r: float(r["TotalDurationNs"]))
+    c, n = counters(d, ks["Name"].split("(")[0].replace("void ", ""))
     avg_ns = float(ks["AverageNs"])
     fetch = 2.0 * c["FETCH_SIZE"] * 1024 if "FETCH_SIZE" in c else None
     write = c["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in c else None
