@@ -2,15 +2,22 @@
 // time-stepping hot path behind the C-ABI of include/h9g.h.
 //
 // Kernel design:
-//   * h9g_year_kernel<L>: one lane = one soil column.  A launch runs one
-//     calendar year: all days x NISURF substeps of HYDROLOGY plus the daily
-//     GROW.  The column's water state lives in VGPRs; its read-mostly data
-//     (soil parameters and their invariants, rootr, the day's constants,
-//     the substep rollback copy) in the lane's column of an LDS block, so
-//     the kernel fits 256 VGPRs (2 waves/SIMD).  HBM traffic per cell-day
-//     is the 7 forcing values (coalesced, cell-fastest) plus the annual
-//     sums (L2-resident) -- the SHARED-state contract of each substep
+//   * h9g_pair_kernel<L, G> (default): one launch runs one calendar year --
+//     all days x NISURF substeps of HYDROLOGY plus the daily GROW -- for
+//     every cell, time innermost as in the reference.  Two lanes per soil
+//     column: the per-layer phases (equilibrium profile, conductivity and
+//     matric potential; ~40 of the ~46 glibc-exact powf of a substep) are
+//     split over the pair and exchanged by DPP, the rest runs in both
+//     lanes.  22 columns per wave, 4 waves per workgroup: 3 waves on every
+//     SIMD at 0.5 deg (767 workgroups, 768 slots).  The column's water
+//     state lives in VGPRs, its read-mostly data (soil parameters and
+//     their invariants, rootr, the day's constants, the substep rollback
+//     copy) in the pair's two columns of an LDS block.  HBM traffic per
+//     cell-day is the 7 forcing values (coalesced, cell-fastest) plus the
+//     annual sums (L2-resident): the SHARED-state contract of each substep
 //     (376 B at L=8) never leaves the CU.
+//   * h9g_solo_kernel<L, G> (H9G_KERNEL=solo): one lane per column, the
+//     same code with one lane doing every layer.
 //   * glibc-exact expf/powf (h9_math.h) read their 32+16-entry tables from
 //     LDS (per-lane indices, no scalar-cache serialisation).
 //   * no MFMA: nothing here is GEMM-shaped.
@@ -41,7 +48,7 @@ static const uint64_t h_exp2tab[32] = H9M_EXP2F_TAB_INIT;
 static const double h_log2tab[32] = H9M_POWF_LOG2_TAB_INIT;
 
 #define H9G_BLOCK 256
-#define H9G_YBLOCK 64   // year kernel: one wave per block (LDS cell stores)
+#define H9G_YBLOCK 64   // solo kernel: one wave per block (LDS cell stores)
 // pair kernel: 22 columns (44 lanes) per wave, 4 waves per workgroup; the
 // 0.5 deg grid is 767 workgroups = 3 waves on each of the 1,024 SIMDs
 #define H9G_PCPW 22
@@ -74,85 +81,6 @@ __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
     l2[t] = c_log2tab[t];
   }
   __syncthreads();
-}
-
-template <int L, class G>
-__global__ void __launch_bounds__(H9G_YBLOCK) __attribute__((amdgpu_waves_per_eu(2, 2))) h9g_year_kernel(const KArgs a, const G g) {
-  __shared__ uint64_t s_e2[32];
-  __shared__ double s_l2[32];
-  __shared__ float s_cell[Lay<L>::N * H9G_YBLOCK];    // cell stores, [field][lane]
-  load_tabs(s_e2, s_l2);
-  const h9m::Tabs T = {s_e2, s_l2};
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.ncell) return;
-  const int n = a.ncell;
-
-  CellStore<L> cs{(lds_float *)&s_cell[threadIdx.x]};
-  St<L> s;
-#pragma unroll
-  for (int f = 0; f < 4 * L + 1; f++) cs.set(f, a.par[(size_t)f * n + c]);
-#pragma unroll
-  for (int i = 1; i <= L; i++) {
-    s.h2o[i] = a.st[(size_t)(0 * L + i - 1) * n + c];
-    s.smp[i] = a.st[(size_t)(2 * L + i - 1) * n + c];
-    cs.set(Lay<L>::ROOTR + i - 1, a.st[(size_t)(3 * L + i - 1) * n + c]);
-  }
-  const size_t o8 = (size_t)(4 * L + 1) * n + c;
-  s.zwt = a.st[o8 + 0 * (size_t)n];
-  s.wa = a.st[o8 + 1 * (size_t)n];
-  s.LAI = a.st[o8 + 2 * (size_t)n];
-  s.LAI_litter = a.st[o8 + 3 * (size_t)n];
-  s.pm = a.st[o8 + 4 * (size_t)n];
-  s.pfm = a.st[o8 + 5 * (size_t)n];
-  s.plen = a.st[o8 + 6 * (size_t)n];
-  s.rdepth = a.st[o8 + 7 * (size_t)n];
-
-  // soil mask (HYBRID9.f90:122-123): SUM(theta_s) > trunc
-  float ts_sum = zero;
-#pragma unroll
-  for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.get(Lay<L>::TS + i - 1);
-  if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
-#pragma unroll
-    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + c] = __builtin_nanf("");
-    return;
-  }
-  cell_inv<L, G>(g, cs);
-  int eday = 0, estep = 0;
-  float errval = 0.0f;
-  const int code = cell_year<L, G>(g, cs, s, a.forc + c, (size_t)n, a.fvar, a.nt, a.nisurf,
-                                   a.grow_on, a.annual + c, (size_t)n, eday, estep, errval, T);
-  int cw = c;            // recompute write-back addresses rather than keep the load ones live
-  opaque(cw);
-  cs.launder();
-
-  // state write-back
-  const size_t ow = (size_t)(4 * L + 1) * n + cw;
-#pragma unroll
-  for (int i = 1; i <= L; i++) {
-    a.st[(size_t)(0 * L + i - 1) * n + cw] = s.h2o[i];
-    a.st[(size_t)(2 * L + i - 1) * n + cw] = s.smp[i];
-    if (a.grow_on) a.st[(size_t)(3 * L + i - 1) * n + cw] = cs.get(Lay<L>::ROOTR + i - 1);
-  }
-  if (a.grow_on) a.st[(size_t)(4 * L) * n + cw] = zero;   // rootr_col(Nlevgrnd)
-  a.st[ow + 0 * (size_t)n] = s.zwt;
-  a.st[ow + 1 * (size_t)n] = s.wa;
-  a.st[ow + 2 * (size_t)n] = s.LAI;
-  a.st[ow + 3 * (size_t)n] = s.LAI_litter;
-  a.st[ow + 4 * (size_t)n] = s.pm;
-  a.st[ow + 5 * (size_t)n] = s.pfm;
-  a.st[ow + 6 * (size_t)n] = s.plen;
-  a.st[ow + 7 * (size_t)n] = s.rdepth;
-
-  if (code) {
-    a.err[0 * (size_t)n + cw] = code;
-    a.err[1 * (size_t)n + cw] = eday;
-    a.err[2 * (size_t)n + cw] = estep;
-    a.err[3 * (size_t)n + cw] = __builtin_bit_cast(int, errval);
-    atomicOr(a.err_flag, 1);
-#pragma unroll
-    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + cw] = __builtin_nanf("");
-    return;
-  }
 }
 
 // Pair kernel (h9g_pair.h): two lanes per soil column, the per-layer powers
@@ -488,8 +416,7 @@ struct h9g_ctx {
   h9g_error last_err{};
   const char *kname = "";
   unsigned *d_stamps = nullptr;   // H9G_STAMPS builds only
-  int kind = 1;        // 1: h9g_pair_kernel (default), 0: h9g_year_kernel (H9G_KERNEL=single),
-                       // 2: h9g_solo_kernel (H9G_KERNEL=solo)
+  int kind = 1;        // 1: h9g_pair_kernel (default), 2: h9g_solo_kernel (H9G_KERNEL=solo)
 };
 
 #define HIPCHK(x)                                                              \
@@ -630,16 +557,13 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     return nullptr;
   }
   static const char *names[3][2][3] = {
-      {{"h9g_year_kernel<8,GeoR>", "h9g_year_kernel<8,GeoC<8,24>>", "h9g_year_kernel<8,GeoC<8,48>>"},
-       {"h9g_year_kernel<10,GeoR>", "h9g_year_kernel<10,GeoC<10,24>>", "h9g_year_kernel<10,GeoC<10,48>>"}},
+      {{"", "", ""}, {"", "", ""}},
       {{"h9g_pair_kernel<8,GeoR>", "h9g_pair_kernel<8,GeoC<8,24>>", "h9g_pair_kernel<8,GeoC<8,48>>"},
        {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}},
       {{"h9g_solo_kernel<8,GeoR>", "h9g_solo_kernel<8,GeoC<8,24>>", "h9g_solo_kernel<8,GeoC<8,48>>"},
        {"h9g_solo_kernel<10,GeoR>", "h9g_solo_kernel<10,GeoC<10,24>>", "h9g_solo_kernel<10,GeoC<10,48>>"}}};
   const char *kenv = getenv("H9G_KERNEL");
-  ctx->kind = 1;
-  if (kenv && strcmp(kenv, "single") == 0) ctx->kind = 0;
-  if (kenv && strcmp(kenv, "solo") == 0) ctx->kind = 2;
+  ctx->kind = (kenv && strcmp(kenv, "solo") == 0) ? 2 : 1;
   const GeoKind gk = geo_kind(*cfg);
   ctx->kname = names[ctx->kind][L == 8 ? 0 : 1][gk == GEO_R ? 0 : (gk == GEO_C24 ? 1 : 2)];
   return ctx;
@@ -806,12 +730,9 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   if (ctx->kind == 2) {
     H9G_DISPATCH(ctx, h9g_solo_kernel, (unsigned)((ctx->n + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
                  ctx->sc, a);
-  } else if (ctx->kind == 1) {
+  } else {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n + per_block - 1) / per_block), 64 * H9G_PWAVES,
-                 ctx->sc, a);
-  } else {
-    H9G_DISPATCH(ctx, h9g_year_kernel, (unsigned)((ctx->n + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
                  ctx->sc, a);
   }
   HIPCHK(hipGetLastError());

@@ -304,8 +304,11 @@ H9K_HD void cell_inv_pair(const G &g, const CS &cs) {
   cs.set_sc(PS_TSDZ1, MAXF(zero, (cs.lay(PF_TS, 1) * g.dz(1))));
 }
 
-// One HYDROLOGY call (HYDROLOGY.f90:141-1283), pair-split.  Same contract
-// as hydrology_step (h9g_step.h), whose comments cite each block.
+// One HYDROLOGY call (/root/reference/SOURCE/HYDROLOGY.f90:141-1283) for
+// one cell; every block cites the reference lines it restates.  Returns 0
+// or an H9G_ERR_* code (the reference's STOP sites) with errval set;
+// theta(1..L) receives the end-of-step volumetric water (:1233).  Under
+// Split2 the per-layer phases are split over the pair (file comment).
 template <int L, class G, class M, class SP, class CS, class PR = NoProf>
 H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta,
                           float &rnf_sum, float &errval, M &m, PR &pr) {

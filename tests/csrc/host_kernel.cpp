@@ -1,5 +1,8 @@
 // TEST INFRASTRUCTURE ONLY: a host (CPU) build of the GPU kernel body
-// hybrid9_amd/csrc/h9g_step.h, used by tests/test_kernel_host.py to pin the
+// (hybrid9_amd/csrc/h9g_pair.h + h9g_step.h, one lane doing every layer:
+// the code of the solo kernel and of the device exact re-run; the pair
+// kernel differs only in which lane evaluates a layer), used by
+// tests/test_kernel_host.py to pin the
 // kernel's arithmetic against the oracle and the reference goldens without
 // a GPU.  Never linked into the product library.
 #include <stdint.h>
@@ -14,66 +17,6 @@ static const double L2[32] = H9M_POWF_LOG2_TAB_INIT;
 
 static int diy(int y) { return y % 4 ? 365 : (y % 100 ? 366 : (y % 400 ? 365 : 366)); }
 
-template <int L, class G>
-static int run_cells(const G &g, int n, int nisurf, int grow_on, int year0, int nyears,
-                     const float *par, const float *forc, float *st, float *ann, int *err) {
-  const h9m::Tabs T = {E2, L2};
-  int ndays = 0;
-  for (int y = 0; y < nyears; y++) ndays += diy(year0 + y);
-  int first = 0;
-#pragma omp parallel for schedule(dynamic, 4)
-  for (int c = 0; c < n; c++) {
-    typedef Lay<L> Y;
-    float store[Y::N];
-    CellStore<L> cs{store};
-    St<L> s;
-    for (int i = 1; i <= L; i++) {
-      cs.set(Y::TS + i - 1, par[0 * n * L + c * L + i - 1]);
-      cs.set(Y::HKS + i - 1, par[1 * n * L + c * L + i - 1]);
-      cs.set(Y::BSW + i - 1, par[2 * n * L + c * L + i - 1]);
-      cs.set(Y::PSI + i - 1, par[3 * n * L + c * L + i - 1]);
-      s.h2o[i] = st[0 * n * L + c * L + i - 1];
-      s.smp[i] = st[2 * n * L + c * L + i - 1];
-      cs.set(Y::ROOTR + i - 1, st[3 * n * L + c * (L + 1) + i - 1]);
-    }
-    cs.set(Y::FMAX, par[4 * n * L + c]);
-    cell_inv<L, G>(g, cs);
-    float *q = st + (size_t)n * (4 * L + 1);
-    s.zwt = q[c]; s.wa = q[n + c]; s.LAI = q[2 * n + c]; s.LAI_litter = q[3 * n + c];
-    s.pm = q[4 * n + c]; s.pfm = q[5 * n + c]; s.plen = q[6 * n + c]; s.rdepth = q[7 * n + c];
-    int d0 = 0;
-    for (int y = 0; y < nyears; y++) {
-      const int nt = diy(year0 + y);
-      float a[12 + L];
-      int eday = 0, estep = 0;
-      float ev = 0;
-      const int code = cell_year<L, G>(g, cs, s, forc + (size_t)d0 * n + c, (size_t)n,
-                                       (size_t)ndays * n, nt, nisurf, grow_on, a, 1, eday,
-                                       estep, ev, T);
-      if (code) {
-        err[4 * c] = code; err[4 * c + 1] = y; err[4 * c + 2] = eday; err[4 * c + 3] = estep;
-#pragma omp atomic write
-        first = code;
-        break;
-      }
-      for (int r = 0; r < 12 + L; r++) ann[((size_t)y * (12 + L) + r) * n + c] = a[r];
-      d0 += nt;
-    }
-    for (int i = 1; i <= L; i++) {
-      st[0 * n * L + c * L + i - 1] = s.h2o[i];
-      st[2 * n * L + c * L + i - 1] = s.smp[i];
-      if (grow_on) st[3 * n * L + c * (L + 1) + i - 1] = cs.get(Y::ROOTR + i - 1);
-    }
-    if (grow_on) st[3 * n * L + c * (L + 1) + L] = 0.0f;
-    q[c] = s.zwt; q[n + c] = s.wa; q[2 * n + c] = s.LAI; q[3 * n + c] = s.LAI_litter;
-    q[4 * n + c] = s.pm; q[5 * n + c] = s.pfm; q[6 * n + c] = s.plen; q[7 * n + c] = s.rdepth;
-  }
-  return first;
-}
-
-// The pair-lane code path (h9g_pair.h) with one lane computing every layer
-// (SplitAll) on a flat per-cell store: the arithmetic of the device pair
-// kernel, checked on the host.
 template <int L, class G>
 static int run_cells_pair(const G &g, int n, int nisurf, int grow_on, int year0, int nyears,
                           const float *par, const float *forc, float *st, float *ann, int *err) {
@@ -132,28 +75,20 @@ static int run_cells_pair(const G &g, int n, int nisurf, int grow_on, int year0,
   return first;
 }
 
+// use_const_geo: 1 = the driver.txt / config-5 layer sets and NISURF 24|48
+// as compile-time geometry (GeoC), 0 = runtime geometry (GeoR).
 extern "C" int h9k_host_run(int n, int L, int nisurf, int grow_on, int year0, int nyears,
                             int use_const_geo, const float *zi, const float *par,
                             const float *forc, float *st, float *ann, int *err) {
-  if (use_const_geo >= 2) {   // pair-lane code path (2: compile-time, 3: runtime geometry)
-    const bool cg = use_const_geo == 2;
+  const bool cg = use_const_geo != 0;
 #define RP(LL, G) return run_cells_pair<LL>(G, n, nisurf, grow_on, year0, nyears, par, forc, st, ann, err)
-    if (L == 8) {
-      if (cg && nisurf == 48) RP(8, (GeoC<8, 48>()));
-      if (cg && nisurf == 24) RP(8, (GeoC<8, 24>()));
-      RP(8, make_geo_r<8>(zi, nisurf));
-    }
-    if (cg && nisurf == 48) RP(10, (GeoC<10, 48>()));
-    if (cg && nisurf == 24) RP(10, (GeoC<10, 24>()));
-    RP(10, make_geo_r<10>(zi, nisurf));
-#undef RP
-  }
   if (L == 8) {
-    if (use_const_geo && nisurf == 48) return run_cells<8>(GeoC<8, 48>(), n, 48, grow_on, year0, nyears, par, forc, st, ann, err);
-    if (use_const_geo && nisurf == 24) return run_cells<8>(GeoC<8, 24>(), n, 24, grow_on, year0, nyears, par, forc, st, ann, err);
-    return run_cells<8>(make_geo_r<8>(zi, nisurf), n, nisurf, grow_on, year0, nyears, par, forc, st, ann, err);
+    if (cg && nisurf == 48) RP(8, (GeoC<8, 48>()));
+    if (cg && nisurf == 24) RP(8, (GeoC<8, 24>()));
+    RP(8, make_geo_r<8>(zi, nisurf));
   }
-  if (use_const_geo && nisurf == 24) return run_cells<10>(GeoC<10, 24>(), n, 24, grow_on, year0, nyears, par, forc, st, ann, err);
-  if (use_const_geo && nisurf == 48) return run_cells<10>(GeoC<10, 48>(), n, 48, grow_on, year0, nyears, par, forc, st, ann, err);
-  return run_cells<10>(make_geo_r<10>(zi, nisurf), n, nisurf, grow_on, year0, nyears, par, forc, st, ann, err);
+  if (cg && nisurf == 48) RP(10, (GeoC<10, 48>()));
+  if (cg && nisurf == 24) RP(10, (GeoC<10, 24>()));
+  RP(10, make_geo_r<10>(zi, nisurf));
+#undef RP
 }

@@ -22,8 +22,11 @@ def _gpu_run(inp, L):
                  grow_on=bool(inp["grow_on"]), state0=inp["state0"])
 
 
+@pytest.mark.parametrize("kernel", ["pair", "solo"])
 @pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit")))
-def test_gpu_matches_reference_golden(name):
+def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
+    """Both year kernels (two lanes per column = the default; one lane)."""
+    monkeypatch.setenv("H9G_KERNEL", kernel)
     meta, inp, exp = load_golden(name)
     out = _gpu_run(inp, meta["L"])
     assert out["rc"] == 0, out["err"]
@@ -31,8 +34,10 @@ def test_gpu_matches_reference_golden(name):
     assert same_bits(out["state"], exp["state"])
 
 
+@pytest.mark.parametrize("kernel", ["pair", "solo"])
 @pytest.mark.parametrize("name", golden_names(kind=("stop",)))
-def test_gpu_reproduces_reference_stop(name):
+def test_gpu_reproduces_reference_stop(name, kernel, monkeypatch):
+    monkeypatch.setenv("H9G_KERNEL", kernel)
     meta, inp, _ = load_golden(name)
     out = _gpu_run(inp, meta["L"])
     s = meta["stop"]
