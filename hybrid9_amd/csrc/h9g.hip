@@ -145,8 +145,9 @@ h9g_pair_kernel(const KArgs a, const G g) {
   float errval = 0.0f;
 #if defined(H9G_STAMPS)
   StampProf pr{stamp_clock(), {0, 0, 0, 0, 0, 0, 0, 0}};
-  const int code = cell_year_pair<L, G>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar, a.nt, a.nisurf,
-                                        a.grow_on, a.annual + c, (size_t)n, eday, estep, errval, T, pr);
+  const int code = cell_year_pair<L, G, Split2, PS, true>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar, a.nt,
+                                                         a.nisurf, a.grow_on, a.annual + c, (size_t)n, eday,
+                                                         estep, errval, T, pr);
   if (lane == 0 && a.stamps)
     for (int k = 0; k < 8; k++) a.stamps[(blockIdx.x * H9G_PWAVES + wave) * 8 + k] = pr.acc[k];
 #else
@@ -236,8 +237,9 @@ h9g_solo_kernel(const KArgs a, const G g) {
   cell_inv_pair<L, G>(g, cs);
   int eday = 0, estep = 0;
   float errval = 0.0f;
-  const int code = cell_year_pair<L, G>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar, a.nt, a.nisurf,
-                                        a.grow_on, a.annual + c, (size_t)n, eday, estep, errval, T);
+  const int code = cell_year_pair<L, G, SplitAll, SS, false>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar,
+                                                             a.nt, a.nisurf, a.grow_on, a.annual + c,
+                                                             (size_t)n, eday, estep, errval, T);
   int cw = c;
   opaque(cw);
   cs.launder();

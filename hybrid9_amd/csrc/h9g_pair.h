@@ -49,7 +49,12 @@ enum : int {
 // per-cell fields
 enum : int {
   PS_FMAX = 0, PS_MH3, PS_TSDZ1, PS_SVZWT, PS_SVWA, PS_SVRNF, PS_SVERR, PS_DAY,
-  PS_N = PS_DAY + D_N
+  PS_LAI = PS_DAY + D_N,               // plant state, parked over the substeps (pair kernel)
+  PS_LAIL, PS_PM, PS_PFM, PS_PLEN, PS_RDEPTH,
+  PS_N
+};
+enum : int {
+  PS_N_NOPARK = PS_LAI                 // per-cell fields of a store that does not park
 };
 
 template <int K>
@@ -132,7 +137,7 @@ struct PairStore {
 // every field in the lane's own column.
 template <int L>
 struct SoloStore {
-  static constexpr int ROWS = PF_N * L + PS_N;
+  static constexpr int ROWS = PF_N * L + PS_N_NOPARK;   // 1054 waves = 5 blocks/CU: no plant parking
   lds_float *b;
   const lds_float *zt;
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
@@ -307,11 +312,12 @@ H9K_HD void cell_inv_pair(const G &g, const CS &cs) {
 // One HYDROLOGY call (/root/reference/SOURCE/HYDROLOGY.f90:141-1283) for
 // one cell; every block cites the reference lines it restates.  Returns 0
 // or an H9G_ERR_* code (the reference's STOP sites) with errval set;
-// theta(1..L) receives the end-of-step volumetric water (:1233).  Under
+// Under
 // Split2 the per-layer phases are split over the pair (file comment).
+// The end-of-step theta(1..L) of :1233 is left to the caller (end_theta).
 template <int L, class G, class M, class SP, class CS, class PR = NoProf>
-H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta,
-                          float &rnf_sum, float &errval, M &m, PR &pr) {
+H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_sum, float &errval,
+                          M &m, PR &pr) {
   constexpr int NT = L / 2;
   const float dt = g.dt();
   constexpr double r1000 = 1.0 / 1000.0;
@@ -319,6 +325,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
 #pragma unroll
   for (int i = 1; i <= L; i++) zim[i] = g.zim(i);
   float *h2o = s.h2o, *smp = s.smp;
+  float theta[L + 1];
   cs.launder();
 #define TS(i) cs.lay(PF_TS, i)
 #define HKS(i) cs.lay(PF_HKS, i)
@@ -744,13 +751,12 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *thet
   }
   h2o[L] = h2o[L] + xs;
   rsub_top = rsub_top - m.div(xs, dt, g.rdt());
-  // :1221-1236
+  // :1221-1236.  The end-of-step theta (:1233) is read only by the daily
+  // sums after the day's last substep (the next substep recomputes theta
+  // from h2osoi_liq, :141-151), so cell_year_pair evaluates it once a day.
   float w1 = ((1.0f - frac_h2osfc) * (qflx_surf + evg + tran) + rsub_top + qflx_rsub_sat) * dt + s.wa;
 #pragma unroll
-  for (int i = 1; i <= L; i++) {
-    w1 = w1 + h2o[i];
-    theta[i] = m.div(MAXF(h2o[i], 1.0E-6f), g.thk(i), g.rthk(i));
-  }
+  for (int i = 1; i <= L; i++) w1 = w1 + h2o[i];
   pr.mark(7);
   // :1244
   if (absf(w1 - w0) > 0.1f) { errval = w1 - w0; return 4; }
@@ -781,11 +787,10 @@ H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const dou
   s.zwt = cs.sc(PS_SVZWT);
   s.wa = cs.sc(PS_SVWA);
   float rnf = cs.sc(PS_SVRNF), errval = zero;
-  float theta[L + 1];
   MathExact me{{e2, l2}};
   const SplitAll sa;
   NoProf np;
-  const int code = hydrology_pair<L, G, MathExact, SplitAll, CS>(*g, cs, sa, s, theta, rnf, errval, me, np);
+  const int code = hydrology_pair<L, G, MathExact, SplitAll, CS>(*g, cs, sa, s, rnf, errval, me, np);
   cs.launder();
 #pragma unroll
   for (int i = 1; i <= L; i++) {
@@ -802,8 +807,8 @@ H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const dou
 // One substep, speculate-then-verify (as substep in h9g_step.h).  A pair
 // re-runs if either of its lanes saw a special-path input.
 template <int L, class G, class SP, class CS, class PR>
-H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta, float &rnf_sum,
-                        float &errval, const h9m::Tabs &T, PR &pr) {
+H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_sum, float &errval,
+                        const h9m::Tabs &T, PR &pr) {
   pr.mark(0);
   save_layers<L>(sp, cs, PF_SVH2O, s.h2o);
   save_layers<L>(sp, cs, PF_SVSMP, s.smp);
@@ -811,7 +816,7 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta,
   cs.set_sc(PS_SVWA, s.wa);
   cs.set_sc(PS_SVRNF, rnf_sum);
   MathFast mf{T, false};
-  int code = hydrology_pair<L, G, MathFast, SP, CS, PR>(g, cs, sp, s, theta, rnf_sum, errval, mf, pr);
+  int code = hydrology_pair<L, G, MathFast, SP, CS, PR>(g, cs, sp, s, rnf_sum, errval, mf, pr);
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
     cs.launder();
     code = substep_exact_pair<L, G, CS>(&g, cs, T.exp2, T.log2);
@@ -820,7 +825,6 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta,
     for (int i = 1; i <= L; i++) {
       s.h2o[i] = cs.lay(PF_SVH2O, i);
       s.smp[i] = cs.lay(PF_SVSMP, i);
-      theta[i] = MAXF(s.h2o[i], 1.0E-6f) / g.thk(i);     // HYDROLOGY.f90:1233
     }
     s.zwt = cs.sc(PS_SVZWT);
     s.wa = cs.sc(PS_SVWA);
@@ -831,7 +835,9 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float *theta,
 }
 
 // One calendar year for one cell (HYBRID9.f90:150-290), as cell_year.
-template <int L, class G, class SP, class CS, class PR = NoProf>
+// Park = keep the plant state in the store over the substeps (register
+// relief for the 168-VGPR pair kernel).
+template <int L, class G, class SP, class CS, bool Park = true, class PR = NoProf>
 H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float *forc, size_t fday,
                           size_t fvar, int nt, int nisurf, int grow_on, float *acc, size_t astride,
                           int &eday, int &estep, float &errval, const h9m::Tabs &T, PR &&pr = PR()) {
@@ -840,11 +846,21 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float
   float *A = acc;
   const size_t as = astride;
   float rnf_sum = zero;
-  float theta[L + 1];
-#pragma unroll
-  for (int i = 1; i <= L; i++) theta[i] = zero;
 #pragma unroll
   for (int k = 0; k < 12 + L; k++) A[k * as] = zero;
+  // plant state parked in the store over the substeps (read by day_consts
+  // and GROW only, once a day)
+  auto park = [&]() __attribute__((always_inline)) {
+    if constexpr (Park) {
+      cs.set_sc(PS_LAI, s.LAI);
+      cs.set_sc(PS_LAIL, s.LAI_litter);
+      cs.set_sc(PS_PM, s.pm);
+      cs.set_sc(PS_PFM, s.pfm);
+      cs.set_sc(PS_PLEN, s.plen);
+      cs.set_sc(PS_RDEPTH, s.rdepth);
+    }
+  };
+  park();
   float npp = zero;
   int code = 0;
   MathExact me{T};
@@ -856,19 +872,33 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float
     {
       const Day d = make_day(f[0 * fvar], f[1 * fvar], f[2 * fvar], f[3 * fvar], f[4 * fvar],
                              f[5 * fvar], f[6 * fvar]);                // :168-184
-      day_consts(d, s.LAI, s.LAI_litter, cs, me);
+      if constexpr (Park)
+        day_consts(d, cs.sc(PS_LAI), cs.sc(PS_LAIL), cs, me);
+      else
+        day_consts(d, s.LAI, s.LAI_litter, cs, me);
     }
     for (int ns = 0; ns < nisurf; ns++) {                            // :193-211
-      code = substep_pair<L, G, SP, CS>(g, cs, sp, s, theta, rnf_sum, errval, T, pr);
+      code = substep_pair<L, G, SP, CS>(g, cs, sp, s, rnf_sum, errval, T, pr);
       if (code) { eday = day; estep = ns; break; }
     }
-    if (code) return code;
     cs.launder();
+    if constexpr (Park) {
+      s.LAI = cs.sc(PS_LAI);
+      s.LAI_litter = cs.sc(PS_LAIL);
+      s.pm = cs.sc(PS_PM);
+      s.pfm = cs.sc(PS_PFM);
+      s.plen = cs.sc(PS_PLEN);
+      s.rdepth = cs.sc(PS_RDEPTH);
+    }
+    if (code) return code;
     opaque(A);
     opaque(f);                 // re-read the day's forcing (not kept live over the substeps)
     const float tas = f[0 * fvar], rlds = f[1 * fvar], rsds = f[2 * fvar], huss = f[3 * fvar];
     const float ps = f[4 * fvar], pr = f[5 * fvar], rhs = f[6 * fvar];
-    if (grow_on) grow_day<L, G, MathExact>(g, tas, s, cs, npp, me);  // :217
+    if (grow_on) {
+      grow_day<L, G, MathExact>(g, tas, s, cs, npp, me);              // :217
+      park();
+    }
     A[A_TAS * as] = A[A_TAS * as] + tas;                              // :235-254
     A[A_RLDS * as] = A[A_RLDS * as] + rlds;
     A[A_RSDS * as] = A[A_RSDS * as] + rsds;
@@ -881,7 +911,8 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float
     float h2o_sum = A[A_H2O * as];
 #pragma unroll
     for (int i = 1; i <= L; i++) {
-      A[(A_THETA + i - 1) * as] = A[(A_THETA + i - 1) * as] + theta[i];
+      const float theta = MAXF(s.h2o[i], 1.0E-6f) / g.thk(i);       // HYDROLOGY.f90:1233
+      A[(A_THETA + i - 1) * as] = A[(A_THETA + i - 1) * as] + theta;
       h2o_sum = h2o_sum + s.h2o[i];
     }
     A[A_H2O * as] = h2o_sum;
