@@ -112,6 +112,12 @@ def lib() -> C.CDLL:
         "h9g_synth_host": (C.c_int, [C.c_uint64, C.c_int, C.c_int, _I64P, _FP, C.c_int,
                                      C.c_int, _FP, _FP]),
         "h9g_land_cells": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint64, _I64P, _FP]),
+        "h9g_write_axy_nc": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, _FP, C.c_int, _I64P, _FP]),
+        "h9g_nc_forcing_read": (C.c_int, [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_int, _I64P,
+                                          C.c_int, C.c_int, _FP]),
+        "h9g_nc_ntimes": (C.c_int, [C.c_char_p]),
+        "h9g_nc_forcing_prefetch": (C.c_int, [vp, C.c_int, C.POINTER(C.c_char_p), C.c_int, C.c_int,
+                                              C.c_int, C.c_int]),
         "h9g_host_expf": (C.c_float, [C.c_float]),
         "h9g_host_powf": (C.c_float, [C.c_float, C.c_float]),
     }
@@ -232,6 +238,12 @@ class Context:
         _check(self._lib.h9g_push_forcing(self._h, slot, forcing.shape[1], _fp(forcing),
                                           int(async_)), "h9g_push_forcing")
 
+    def nc_prefetch(self, slot: int, paths, nx: int, ny: int, t0: int, nt: int):
+        """Async PGF prefetch from NetCDF files (READ_PGF.f90) into `slot`:
+        days [t0, t0+nt) of the 7 files, needs set_cells."""
+        _check(self._lib.h9g_nc_forcing_prefetch(self._h, slot, _paths(paths), nx, ny, t0, nt),
+               "h9g_nc_forcing_prefetch")
+
     def push_forcing_device(self, slot: int, nday: int, dev_ptr: int):
         _check(self._lib.h9g_push_forcing_device(self._h, slot, nday, C.c_void_p(dev_ptr)),
                "h9g_push_forcing_device")
@@ -286,6 +298,47 @@ class Context:
 
     def kernel_name(self) -> str:
         return self._lib.h9g_kernel_name(self._h).decode()
+
+
+PGF_VARS = ("tas", "rlds", "rsds", "huss", "ps", "pr", "rhs")   # READ_PGF.f90 order
+
+
+def _paths(paths):
+    paths = [str(p).encode() for p in paths]
+    if len(paths) != NFORCING:
+        raise ValueError("need the 7 PGF files in READ_PGF order " + " ".join(PGF_VARS))
+    return (C.c_char_p * NFORCING)(*paths)
+
+
+def pgf_paths(directory, decade: str, suffix: str = "nc4"):
+    """READ_PGF.f90:22-106 file names: <var>_pgfv2.1_<decade>.<suffix>."""
+    return [str(Path(directory) / f"{v}_pgfv2.1_{decade}.{suffix}") for v in PGF_VARS]
+
+
+def nc_ntimes(path) -> int:
+    """NTIMES of a PGF file (its 'time' dimension, READ_NET_CDF_0D.f90)."""
+    return _check(lib().h9g_nc_ntimes(str(path).encode()), "h9g_nc_ntimes")
+
+
+def nc_forcing_read(paths, nx: int, ny: int, gid, t0: int, nt: int) -> np.ndarray:
+    """Days [t0, t0+nt) of the 7 PGF files at grid ids gid -> (7, nt, ncell)."""
+    gid = np.ascontiguousarray(gid, dtype=np.int64)
+    out = np.empty((NFORCING, nt, gid.size), dtype=np.float32)
+    _check(lib().h9g_nc_forcing_read(_paths(paths), nx, ny, gid.size, gid.ctypes.data_as(_I64P), t0, nt,
+                                     _fp(out)), "h9g_nc_forcing_read")
+    return out
+
+
+def write_axy_nc(path, annual, gid, zc, nx: int = 720, ny: int = 360):
+    """WRITE_NET_CDF_3DR.f90: one year of annual means (12+L, ncell) of the
+    cells gid to axyYYYY.nc (netCDF classic, the reference's schema)."""
+    annual = np.ascontiguousarray(annual, dtype=np.float32)
+    gid = np.ascontiguousarray(gid, dtype=np.int64)
+    zc = np.ascontiguousarray(zc, dtype=np.float32)
+    L = annual.shape[0] - 12
+    assert annual.shape[1] == gid.size and zc.size == L
+    _check(lib().h9g_write_axy_nc(str(path).encode(), nx, ny, L, _fp(zc), gid.size,
+                                  gid.ctypes.data_as(_I64P), _fp(annual)), "h9g_write_axy_nc")
 
 
 def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=True,

@@ -16,7 +16,8 @@ from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 SRC = HERE / "csrc" / "h9g.hip"
-DEPS = [SRC, HERE / "csrc" / "h9_math.h", HERE / "csrc" / "h9g_step.h",
+SRC_IO = HERE / "csrc" / "h9g_io.cpp"       # host-only NetCDF I/O
+DEPS = [SRC, SRC_IO, HERE / "csrc" / "h9_math.h", HERE / "csrc" / "h9g_step.h",
         HERE / "csrc" / "h9g_synth.h", HERE / "csrc" / "h9g_geo.h",
         HERE / "csrc" / "h9g_pair.h",
         HERE.parent / "include" / "h9g.h"]
@@ -47,7 +48,7 @@ def build(force: bool = False, verbose: bool = False, extra=()) -> Path:
         return OUT
     OUT.parent.mkdir(parents=True, exist_ok=True)
     tmp = OUT.with_suffix(".so.tmp")
-    cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *extra, str(SRC), "-o", str(tmp)]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *extra, str(SRC), str(SRC_IO), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
 
 #include "../../include/h9g.h"
@@ -418,6 +419,10 @@ struct h9g_ctx {
   h9g_error last_err{};
   const char *kname = "";
   unsigned *d_stamps = nullptr;   // H9G_STAMPS builds only
+  std::vector<int64_t> h_gid;     // grid ids of the cells (h9g_set_cells), for NetCDF ingest
+  std::vector<float *> h_pin;     // per-slot pinned staging of the NetCDF prefetch
+  std::vector<std::thread> prefetch;
+  std::vector<int> prefetch_rc;
   int kind = 1;        // 1: h9g_pair_kernel (default), 2: h9g_solo_kernel (H9G_KERNEL=solo)
 };
 
@@ -490,6 +495,8 @@ int h9g_state_size(int nlayers) { return 4 * nlayers + 9; }
 
 void h9g_destroy(h9g_ctx *ctx) {
   if (!ctx) return;
+  for (auto &t : ctx->prefetch)
+    if (t.joinable()) t.join();
   (void)hipSetDevice(ctx->device);
   if (ctx->sc) hipStreamSynchronize(ctx->sc);
   if (ctx->sx) hipStreamSynchronize(ctx->sx);
@@ -509,6 +516,7 @@ void h9g_destroy(h9g_ctx *ctx) {
     (void)hipEventDestroy(ctx->ev0[i]);
     (void)hipEventDestroy(ctx->ev1[i]);
   }
+  for (auto p : ctx->h_pin) (void)hipHostFree(p);
   if (ctx->sc) hipStreamDestroy(ctx->sc);
   if (ctx->sx) hipStreamDestroy(ctx->sx);
   delete ctx;
@@ -546,6 +554,9 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
          hipMemset(ctx->d_ann, 0xff, sizeof(float) * (12 + L) * n) == hipSuccess;
   }
   ctx->slot_days.assign(cfg->nslots, 0);
+  ctx->h_pin.assign(cfg->nslots, nullptr);
+  ctx->prefetch.resize(cfg->nslots);
+  ctx->prefetch_rc.assign(cfg->nslots, 0);
   ctx->ev_copied.resize(cfg->nslots);
   ctx->ev_consumed.resize(cfg->nslots);
   for (int s = 0; ok && s < cfg->nslots; s++)
@@ -692,9 +703,18 @@ int h9g_push_forcing_device(h9g_ctx *ctx, int slot, int nday, const float *dev_f
   return push_impl(ctx, slot, nday, dev_forcing, hipMemcpyDeviceToDevice, true);
 }
 
+// Join the NetCDF prefetch thread of a slot (its copy is queued when it ends).
+static int join_prefetch(h9g_ctx *ctx, int slot) {
+  if (ctx->prefetch[slot].joinable()) ctx->prefetch[slot].join();
+  const int rc = ctx->prefetch_rc[slot];
+  ctx->prefetch_rc[slot] = 0;
+  return rc;
+}
+
 int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   if (!ctx || slot < 0 || slot >= ctx->cfg.nslots || jyear < 1861 || jyear > 2299) return H9G_EINVAL;
   if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
+  if (const int prc = join_prefetch(ctx, slot)) return prc;
   const int nt = days_in_year(jyear);
   if (ctx->slot_days[slot] < nt) return H9G_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
@@ -821,6 +841,7 @@ int h9g_get_diagnostics(h9g_ctx *ctx, double *host_out, double *dev_out) {
 
 int h9g_set_cells(h9g_ctx *ctx, const int64_t *gid, const float *lat) {
   if (!ctx || !gid || !lat) return H9G_EINVAL;
+  ctx->h_gid.assign(gid, gid + ctx->n);
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipMemcpy(ctx->d_gid, gid, sizeof(int64_t) * ctx->n, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(ctx->d_lat, lat, sizeof(float) * ctx->n, hipMemcpyHostToDevice));
@@ -853,6 +874,36 @@ int h9g_synth_forcing(h9g_ctx *ctx, int slot, uint64_t seed, int day0, int nday)
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev_copied[slot], ctx->sx));
   ctx->slot_days[slot] = nday;
+  return 0;
+}
+
+// Async PGF prefetch (READ_PGF.f90 on a host thread): days [t0, t0+nt) of
+// the 7 NetCDF files are gathered for the context's cells (h9g_set_cells)
+// into the slot's pinned staging buffer, then copied into the slot on the
+// copy stream.  h9g_run_year on that slot joins the thread first, so the
+// read of year y+1 overlaps the kernel of year y.
+int h9g_nc_forcing_prefetch(h9g_ctx *ctx, int slot, const char *const *paths, int nx, int ny, int t0, int nt) {
+  if (!ctx || slot < 0 || slot >= ctx->cfg.nslots || !paths || nt < 1 || nt > ctx->cfg.max_days || t0 < 0)
+    return H9G_EINVAL;
+  if (ctx->h_gid.size() != ctx->n) return H9G_ESTATE;
+  for (int k = 0; k < H9G_NFORCING; k++)
+    if (!paths[k]) return H9G_EINVAL;
+  if (const int prc = join_prefetch(ctx, slot)) return prc;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t n = ctx->n;
+  if (!ctx->h_pin[slot])
+    HIPCHK(hipHostMalloc(&ctx->h_pin[slot], sizeof(float) * 7 * (size_t)ctx->cfg.max_days * n, hipHostMallocDefault));
+  // the staging buffer may still feed the slot's previous copy
+  HIPCHK(hipEventSynchronize(ctx->ev_copied[slot]));
+  std::vector<std::string> p(paths, paths + H9G_NFORCING);
+  ctx->slot_days[slot] = nt;
+  ctx->prefetch[slot] = std::thread([ctx, slot, p, nx, ny, t0, nt]() {
+    const char *pp[H9G_NFORCING];
+    for (int k = 0; k < H9G_NFORCING; k++) pp[k] = p[k].c_str();
+    int rc = h9g_nc_forcing_read(pp, nx, ny, (int)ctx->n, ctx->h_gid.data(), t0, nt, ctx->h_pin[slot]);
+    if (rc == 0) rc = push_impl(ctx, slot, nt, ctx->h_pin[slot], hipMemcpyHostToDevice, true);
+    ctx->prefetch_rc[slot] = rc;
+  });
   return 0;
 }
 

@@ -1,0 +1,428 @@
+// h9g_io.cpp -- NetCDF I/O of the hot path's inputs and outputs (host C++,
+// part of libh9g.so), SURVEY.md §8f rows 1-2:
+//
+//   * forcing ingest, /root/reference/SOURCE/READ_PGF.f90:22-109 and
+//     READ_NET_CDF_3DR.f90:43-98: one file per PGF variable (tas rlds rsds
+//     huss ps pr rhs), the variable's 4th netCDF variable (varid = 4,
+//     READ_PGF.f90:30) with dims (time, lat, lon) -- Fortran (lon,lat,time)
+//     -- and NTIMES from the 'time' dimension (READ_NET_CDF_3DR.f90:48-52).
+//     h9g_nc_forcing_read gathers the land cells of a context for a range
+//     of days; h9g_nc_forcing_prefetch does it on a host thread into pinned
+//     memory and queues the copy into a forcing slot (async PGF prefetch).
+//   * annual output, WRITE_NET_CDF_3DR.f90:93-263: axyYYYY.nc with the same
+//     dimensions (latitude, longitude, layer_centre_depth), coordinate
+//     variables, variable names, units and NaN _FillValue.
+//
+// Format: netCDF "classic" (CDF-1) and 64-bit-offset (CDF-2) files, read
+// and written directly (the format is a big-endian header followed by
+// the variables' data; record variables are interleaved per record).  The
+// reference writes netCDF-4/HDF5 (NF90_NETCDF4, :93); no HDF5 or netCDF
+// library exists in this image, so output is CDF-2 with the identical
+// schema, readable by every netCDF tool (and scipy.io.netcdf_file), and
+// input is CDF-1/2 (PGF .nc4 converts with `nccopy -k 64-bit-offset`).
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <cmath>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/h9g.h"
+
+namespace {
+
+enum { NC_BYTE = 1, NC_CHAR = 2, NC_SHORT = 3, NC_INT = 4, NC_FLOAT = 5, NC_DOUBLE = 6 };
+enum { TAG_DIM = 0x0A, TAG_VAR = 0x0B, TAG_ATT = 0x0C };
+
+int type_size(int t) {
+  switch (t) {
+    case NC_BYTE: case NC_CHAR: return 1;
+    case NC_SHORT: return 2;
+    case NC_INT: case NC_FLOAT: return 4;
+    case NC_DOUBLE: return 8;
+  }
+  return 0;
+}
+size_t pad4(size_t n) { return (n + 3) & ~(size_t)3; }
+
+// ------------------------------------------------------------------ reader
+struct NcVar {
+  std::string name;
+  std::vector<int> dims;
+  int type = 0;
+  uint64_t vsize = 0, begin = 0;
+  bool record = false;
+};
+
+struct NcReader {
+  FILE *f = nullptr;
+  int version = 0;
+  uint64_t numrecs = 0, recsize = 0;
+  std::vector<std::string> dim_names;
+  std::vector<uint64_t> dim_len;
+  int rec_dim = -1;
+  std::vector<NcVar> vars;
+  std::vector<unsigned char> hdr;
+  size_t pos = 0;
+  bool ok = true;
+
+  ~NcReader() {
+    if (f) fclose(f);
+  }
+  uint32_t u32() {
+    if (pos + 4 > hdr.size()) { ok = false; return 0; }
+    const unsigned char *p = &hdr[pos];
+    pos += 4;
+    return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+  }
+  uint64_t u64() {
+    const uint64_t hi = u32();
+    return hi << 32 | u32();
+  }
+  std::string name() {
+    const uint32_t n = u32();
+    if (!ok || pos + n > hdr.size()) { ok = false; return ""; }
+    std::string s((const char *)&hdr[pos], n);
+    pos += pad4(n);
+    return s;
+  }
+  void skip_atts() {
+    const uint32_t tag = u32(), n = u32();
+    if (tag == 0 && n == 0) return;
+    if (tag != TAG_ATT) { ok = false; return; }
+    for (uint32_t a = 0; a < n && ok; a++) {
+      name();
+      const int t = (int)u32();
+      const uint32_t nel = u32();
+      pos += pad4((size_t)nel * type_size(t));
+    }
+  }
+  bool open(const char *path) {
+    f = fopen(path, "rb");
+    if (!f) return false;
+    hdr.resize(1 << 16);
+    size_t got = fread(hdr.data(), 1, hdr.size(), f);
+    // grow until the header parses (headers are small; PGF: < 4 KiB)
+    for (;;) {
+      hdr.resize(got);
+      pos = 0;
+      ok = true;
+      if (parse()) return true;
+      if (got < (size_t)1 << 16 || hdr.size() > ((size_t)1 << 26)) return false;
+      const size_t want = hdr.size() * 4;
+      hdr.resize(want);
+      fseek(f, 0, SEEK_SET);
+      got = fread(hdr.data(), 1, want, f);
+    }
+  }
+  bool parse() {
+    if (hdr.size() < 8 || memcmp(hdr.data(), "CDF", 3) != 0) return false;
+    version = hdr[3];
+    if (version != 1 && version != 2) return false;
+    pos = 4;
+    numrecs = u32();
+    uint32_t tag = u32(), n = u32();
+    dim_names.clear();
+    dim_len.clear();
+    rec_dim = -1;
+    if (tag == TAG_DIM) {
+      for (uint32_t d = 0; d < n && ok; d++) {
+        dim_names.push_back(name());
+        dim_len.push_back(u32());
+        if (dim_len.back() == 0) rec_dim = (int)d;
+      }
+    } else if (tag != 0 || n != 0) {
+      return false;
+    }
+    skip_atts();                                  // global attributes
+    tag = u32();
+    n = u32();
+    vars.clear();
+    if (tag == TAG_VAR) {
+      for (uint32_t v = 0; v < n && ok; v++) {
+        NcVar var;
+        var.name = name();
+        const uint32_t nd = u32();
+        for (uint32_t k = 0; k < nd && ok; k++) var.dims.push_back((int)u32());
+        skip_atts();
+        var.type = (int)u32();
+        var.vsize = u32();
+        var.begin = version == 2 ? u64() : u32();
+        var.record = !var.dims.empty() && var.dims[0] == rec_dim;
+        vars.push_back(var);
+      }
+    } else if (tag != 0 || n != 0) {
+      return false;
+    }
+    if (!ok) return false;
+    recsize = 0;
+    int nrecvars = 0;
+    for (auto &v : vars)
+      if (v.record) { recsize += v.vsize; nrecvars++; }
+    if (nrecvars == 1) {                          // a single record variable is not padded
+      for (auto &v : vars)
+        if (v.record) {
+          uint64_t sz = type_size(v.type);
+          for (size_t k = 1; k < v.dims.size(); k++) sz *= dim_len[v.dims[k]];
+          recsize = sz;
+        }
+    }
+    return true;
+  }
+  uint64_t dim_of(const NcVar &v, size_t k) const {
+    const int d = v.dims[k];
+    return d == rec_dim ? numrecs : dim_len[d];
+  }
+  // float data of v at first-dimension index t (all remaining dims)
+  bool read_slice(const NcVar &v, uint64_t t, float *out) {
+    if (v.type != NC_FLOAT || v.dims.empty()) return false;
+    uint64_t n = 1;
+    for (size_t k = 1; k < v.dims.size(); k++) n *= dim_of(v, k);
+    const uint64_t off = v.record ? v.begin + t * recsize : v.begin + t * n * 4;
+    if (fseeko(f, (off_t)off, SEEK_SET) != 0) return false;
+    if (fread(out, 4, n, f) != n) return false;
+    uint32_t *u = (uint32_t *)out;
+    for (uint64_t i = 0; i < n; i++) u[i] = __builtin_bswap32(u[i]);
+    return true;
+  }
+  const NcVar *find(const char *nm) const {
+    for (auto &v : vars)
+      if (v.name == nm) return &v;
+    return nullptr;
+  }
+  int dim_index(const char *nm) const {
+    for (size_t d = 0; d < dim_names.size(); d++)
+      if (dim_names[d] == nm) return (int)d;
+    return -1;
+  }
+};
+
+// ------------------------------------------------------------------ writer
+struct Att {
+  std::string name;
+  int type;
+  std::vector<unsigned char> be;   // big-endian payload
+  uint32_t nel;
+};
+struct WVar {
+  std::string name;
+  std::vector<int> dims;
+  std::vector<Att> atts;
+  uint64_t nel = 0, begin = 0;
+};
+
+struct Buf {
+  std::vector<unsigned char> b;
+  void u32(uint32_t x) {
+    unsigned char c[4] = {(unsigned char)(x >> 24), (unsigned char)(x >> 16), (unsigned char)(x >> 8),
+                          (unsigned char)x};
+    b.insert(b.end(), c, c + 4);
+  }
+  void u64(uint64_t x) {
+    u32((uint32_t)(x >> 32));
+    u32((uint32_t)x);
+  }
+  void pad() {
+    while (b.size() % 4) b.push_back(0);
+  }
+  void name(const std::string &s) {
+    u32((uint32_t)s.size());
+    b.insert(b.end(), s.begin(), s.end());
+    pad();
+  }
+};
+
+Att text_att(const char *name, const char *v) {
+  Att a{name, NC_CHAR, {}, (uint32_t)strlen(v)};
+  a.be.assign(v, v + strlen(v));
+  return a;
+}
+Att float_att(const char *name, float v) {
+  Att a{name, NC_FLOAT, {}, 1};
+  uint32_t u;
+  memcpy(&u, &v, 4);
+  a.be = {(unsigned char)(u >> 24), (unsigned char)(u >> 16), (unsigned char)(u >> 8), (unsigned char)u};
+  return a;
+}
+
+// CDF-2 file with fixed-size float variables; data(v, out) fills v's values.
+template <class F>
+int write_cdf2(const char *path, const std::vector<std::pair<std::string, uint32_t>> &dims,
+               std::vector<WVar> &vars, F data) {
+  auto header = [&]() {
+    Buf h;
+    h.b = {'C', 'D', 'F', 2};
+    h.u32(0);                                    // numrecs
+    h.u32(TAG_DIM);
+    h.u32((uint32_t)dims.size());
+    for (auto &d : dims) {
+      h.name(d.first);
+      h.u32(d.second);
+    }
+    h.u32(0);                                    // no global attributes
+    h.u32(0);
+    h.u32(TAG_VAR);
+    h.u32((uint32_t)vars.size());
+    for (auto &v : vars) {
+      h.name(v.name);
+      h.u32((uint32_t)v.dims.size());
+      for (int d : v.dims) h.u32((uint32_t)d);
+      if (v.atts.empty()) {
+        h.u32(0);
+        h.u32(0);
+      } else {
+        h.u32(TAG_ATT);
+        h.u32((uint32_t)v.atts.size());
+        for (auto &a : v.atts) {
+          h.name(a.name);
+          h.u32((uint32_t)a.type);
+          h.u32(a.nel);
+          h.b.insert(h.b.end(), a.be.begin(), a.be.end());
+          h.pad();
+        }
+      }
+      h.u32(NC_FLOAT);
+      const uint64_t vs = pad4(v.nel * 4);
+      h.u32(vs > 0xffffffffu ? 0xffffffffu : (uint32_t)vs);
+      h.u64(v.begin);
+    }
+    return h;
+  };
+  Buf h = header();                              // sizes first, then the real begins
+  uint64_t off = h.b.size();
+  for (auto &v : vars) {
+    v.begin = off;
+    off += pad4(v.nel * 4);
+  }
+  h = header();
+  FILE *f = fopen(path, "wb");
+  if (!f) return H9G_EINVAL;
+  bool ok = fwrite(h.b.data(), 1, h.b.size(), f) == h.b.size();
+  std::vector<float> tmp;
+  for (size_t k = 0; ok && k < vars.size(); k++) {
+    tmp.assign(vars[k].nel, 0.0f);
+    data(k, tmp.data());
+    uint32_t *u = (uint32_t *)tmp.data();
+    for (uint64_t i = 0; i < vars[k].nel; i++) u[i] = __builtin_bswap32(u[i]);
+    ok = fwrite(tmp.data(), 4, vars[k].nel, f) == vars[k].nel;
+  }
+  ok = (fclose(f) == 0) && ok;
+  return ok ? 0 : H9G_EINVAL;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------- C-ABI
+extern "C" {
+
+// WRITE_NET_CDF_3DR.f90: one year of annual means of the cells `gid`
+// (grid ids iy*nx+ix, latitude row iy from the north, INIT.f90:142-145) to
+// a CDF-2 file; every other grid cell is the NaN fill.
+int h9g_write_axy_nc(const char *path, int nx, int ny, int nlayers, const float *zc, int ncell,
+                     const int64_t *gid, const float *annual) {
+  if (!path || nx <= 0 || ny <= 0 || nlayers < 1 || nlayers > H9G_LMAX || ncell < 0 || (ncell && (!gid || !annual)))
+    return H9G_EINVAL;
+  const int L = nlayers;
+  for (int c = 0; c < ncell; c++)
+    if (gid[c] < 0 || gid[c] >= (int64_t)nx * ny) return H9G_EINVAL;
+  const float nan = std::nanf("");
+  // dims in definition order (WRITE_NET_CDF_3DR.f90:101-103)
+  const std::vector<std::pair<std::string, uint32_t>> dims = {
+      {"latitude", (uint32_t)ny}, {"longitude", (uint32_t)nx}, {"layer_centre_depth", (uint32_t)L}};
+  enum { D_LAT = 0, D_LON = 1, D_Z = 2 };
+  // (name, units, annual row) of the 2-D fields (:53-77, :142-180)
+  struct F2 { const char *name, *units; int row; };
+  const F2 f2[] = {{"net primary production", "g[DM]/m^2/yr", 0},
+                   {"plant mass", "g[DM]", 1},
+                   {"runoff", "mm/s", 2},
+                   {"evaporation", "mm/s", 3},
+                   {"temperature", "K", 4},
+                   {"specific_humidity", "kg[water]/kg[air]", 7},
+                   {"air_pressure", "Pa", 8},
+                   {"precipitation", "kg/m^2/s", 9},
+                   {"relative_humidity", "percent", 10},
+                   {"soil_water", "mm", 11 + L}};
+  std::vector<WVar> vars;
+  vars.push_back({"latitude", {D_LAT}, {text_att("units", "degrees_north")}, (uint64_t)ny});
+  vars.push_back({"longitude", {D_LON}, {text_att("units", "degrees_east")}, (uint64_t)nx});
+  vars.push_back({"layer_centre_depth", {D_Z}, {text_att("units", "mm")}, (uint64_t)L});
+  for (const F2 &v : f2)
+    vars.push_back({v.name, {D_LAT, D_LON}, {text_att("units", v.units), float_att("_FillValue", nan)},
+                    (uint64_t)nx * ny});
+  vars.push_back({"soil_water_layers", {D_LAT, D_LON, D_Z},
+                  {text_att("units", "mm^3/mm^3"), float_att("_FillValue", nan)}, (uint64_t)nx * ny * L});
+  const float dlon = 360.0f / (float)nx, dlat = 180.0f / (float)ny;
+  return write_cdf2(path, dims, vars, [&](size_t k, float *out) {
+    const uint64_t n = vars[k].nel;
+    if (k == 0) {                                // INIT.f90:145 lat_all(y) = 89.75 - (y-1)*0.5
+      for (int y = 0; y < ny; y++) out[y] = (90.0f - 0.5f * dlat) - (float)y * dlat;
+    } else if (k == 1) {                         // INIT.f90:142 lon_all(x) = -179.75 + (x-1)*0.5
+      for (int x = 0; x < nx; x++) out[x] = (-180.0f + 0.5f * dlon) + (float)x * dlon;
+    } else if (k == 2) {                         // zc_o (INIT.f90:262)
+      for (int i = 0; i < L; i++) out[i] = zc ? zc[i] : nan;
+    } else if (k < 3 + sizeof(f2) / sizeof(f2[0])) {
+      for (uint64_t i = 0; i < n; i++) out[i] = nan;
+      const int row = f2[k - 3].row;
+      for (int c = 0; c < ncell; c++) out[gid[c]] = annual[(size_t)row * ncell + c];
+    } else {                                     // soil_water_layers (lat, lon, z)
+      for (uint64_t i = 0; i < n; i++) out[i] = nan;
+      for (int c = 0; c < ncell; c++)
+        for (int i = 0; i < L; i++) out[(size_t)gid[c] * L + i] = annual[(size_t)(11 + i) * ncell + c];
+    }
+  });
+}
+
+// READ_PGF.f90 + READ_NET_CDF_3DR.f90 for the cells of a context: days
+// [t0, t0+nt) of the 7 files (READ_PGF order tas rlds rsds huss ps pr rhs),
+// variable 4 of each (dims time, lat, lon), gathered at the grid ids gid
+// into out (7, nt, ncell).  The 7 files are read on 7 host threads.
+int h9g_nc_forcing_read(const char *const *paths, int nx, int ny, int ncell, const int64_t *gid, int t0,
+                        int nt, float *out) {
+  if (!paths || nx <= 0 || ny <= 0 || ncell <= 0 || !gid || t0 < 0 || nt < 1 || !out) return H9G_EINVAL;
+  int rc[H9G_NFORCING];
+  std::vector<std::thread> th;
+  for (int k = 0; k < H9G_NFORCING; k++) {
+    rc[k] = 0;
+    th.emplace_back([&, k]() {
+      NcReader r;
+      if (!paths[k] || !r.open(paths[k]) || r.vars.empty()) { rc[k] = H9G_EINVAL; return; }
+      // varid = 4 (READ_PGF.f90:30) when it is the (time, lat, lon) float
+      // field, as in the PGF files; otherwise the file's only such field
+      const int dt = r.dim_index("time");
+      auto is_field = [&](const NcVar &x) { return x.type == NC_FLOAT && x.dims.size() == 3 && x.dims[0] == dt; };
+      const NcVar *pv = &r.vars[r.vars.size() >= 4 ? 3 : 0];
+      if (!is_field(*pv))
+        for (auto &x : r.vars)
+          if (is_field(x)) { pv = &x; break; }
+      const NcVar &v = *pv;
+      if (v.type != NC_FLOAT || v.dims.size() != 3 || v.dims[0] != dt || r.dim_of(v, 1) != (uint64_t)ny ||
+          r.dim_of(v, 2) != (uint64_t)nx || (uint64_t)(t0 + nt) > r.dim_of(v, 0)) {
+        rc[k] = H9G_EINVAL;
+        return;
+      }
+      std::vector<float> slice((size_t)nx * ny);
+      for (int t = 0; t < nt; t++) {
+        if (!r.read_slice(v, (uint64_t)(t0 + t), slice.data())) { rc[k] = H9G_EINVAL; return; }
+        float *o = out + ((size_t)k * nt + t) * ncell;
+        for (int c = 0; c < ncell; c++) o[c] = slice[(size_t)gid[c]];
+      }
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int k = 0; k < H9G_NFORCING; k++)
+    if (rc[k]) return rc[k];
+  return 0;
+}
+
+// NTIMES of a PGF file (READ_NET_CDF_0D.f90: the 'time' dimension).
+int h9g_nc_ntimes(const char *path) {
+  NcReader r;
+  if (!path || !r.open(path)) return H9G_EINVAL;
+  const int d = r.dim_index("time");
+  if (d < 0) return H9G_EINVAL;
+  return d == r.rec_dim ? (int)r.numrecs : (int)r.dim_len[d];
+}
+
+}  // extern "C"

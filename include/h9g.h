@@ -142,6 +142,26 @@ int h9g_synth_params(h9g_ctx *ctx, uint64_t seed);
 int h9g_synth_forcing(h9g_ctx *ctx, int slot, uint64_t seed, int day0,
                       int nday);
 
+/* --- NetCDF I/O (hybrid9_amd/csrc/h9g_io.cpp; classic CDF-1/2 files) --- */
+/* WRITE_NET_CDF_3DR.f90:93-263: annual means (h9g_get_annual layout, 12+L
+ * rows of ncell) of the cells gid (grid ids iy*nx+ix, row iy from the
+ * north) to axyYYYY.nc with the reference's dimensions, variable names,
+ * units and NaN _FillValue; zc = layer centre depths (L).  Host only. */
+int h9g_write_axy_nc(const char *path, int nx, int ny, int nlayers,
+                     const float *zc, int ncell, const int64_t *gid,
+                     const float *annual);
+/* READ_PGF.f90 / READ_NET_CDF_3DR.f90: days [t0, t0+nt) of variable 4
+ * (time, lat, lon) of the 7 PGF files (tas rlds rsds huss ps pr rhs)
+ * gathered at the grid ids gid into out (7, nt, ncell).  Host only. */
+int h9g_nc_forcing_read(const char *const *paths, int nx, int ny, int ncell,
+                        const int64_t *gid, int t0, int nt, float *out);
+/* NTIMES of a PGF file: length of its 'time' dimension. */
+int h9g_nc_ntimes(const char *path);
+/* The same read on a host thread into pinned memory, then an async copy
+ * into `slot` (needs h9g_set_cells); h9g_run_year on the slot waits. */
+int h9g_nc_forcing_prefetch(h9g_ctx *ctx, int slot, const char *const *paths,
+                            int nx, int ny, int t0, int nt);
+
 /* --- measurement ------------------------------------------------------ */
 /* Device time (HIP events on the compute stream) of the last year kernel,
  * and of all year kernels since the last reset. */

@@ -156,3 +156,49 @@ def test_async_prefetch_pipeline():
         st = ctx.get_state()
     assert same_bits(ann, exp["annual"][1])
     assert same_bits(st, exp["state"])
+
+
+def test_netcdf_prefetch_pipeline(tmp_path):
+    """READ_PGF path from NetCDF files: the async prefetch (host thread ->
+    pinned staging -> copy stream, h9g_nc_forcing_prefetch) of two years of
+    PGF-layout files gives the same results as pushing the same forcing
+    directly, and the annual output written as axyYYYY.nc reads back equal."""
+    from scipy.io import netcdf_file
+    from tests.test_netcdf import write_pgf_like
+    nx, ny, nland = 24, 12, 60
+    gid, lat = synth.land_cells(nx, ny, nland), None
+    lat = synth.cell_lat(gid, nx, ny)
+    params = synth.make_params(gid, 8)
+    nt = synth.days_in_year(1903) + synth.days_in_year(1904)
+    f = synth.make_forcing(gid, lat, synth.year_day0(1903), nt)          # (7, nt, ncell)
+    full = np.full((7, nt, ny * nx), np.float32(250.0))
+    full[:, :, gid] = f
+    paths = [write_pgf_like(tmp_path, v, full[k].reshape(nt, ny, nx), 2) for k, v in enumerate(h.PGF_VARS)]
+    d0 = synth.days_in_year(1903)
+
+    def run(prefetch):
+        with h.Context(nland, synth.ZI_L8, nisurf=48) as ctx:
+            ctx.set_cells(gid, lat)
+            ctx.set_params(params)
+            ctx.init_state()
+            if prefetch:
+                ctx.nc_prefetch(0, paths, nx, ny, 0, d0)
+                ctx.nc_prefetch(1, paths, nx, ny, d0, nt - d0)
+            else:
+                ctx.push_forcing(0, f[:, :d0])
+                ctx.push_forcing(1, f[:, d0:])
+            ctx.run_year(0, 1903)
+            ctx.run_year(1, 1904)
+            ctx.sync()
+            return ctx.get_annual(), ctx.get_state()
+
+    a1, s1 = run(True)
+    a0, s0 = run(False)
+    assert same_bits(a1, a0) and same_bits(s1, s0)
+    out = tmp_path / "axy1904.nc"
+    zc = np.array([synth.ZI_L8[i] - (synth.ZI_L8[i] - synth.ZI_L8[i - 1]) / np.float32(2)
+                   for i in range(1, 9)], np.float32)
+    h.write_axy_nc(out, a1, gid, zc, nx, ny)
+    with netcdf_file(out, "r", mmap=False) as nc:
+        assert same_bits(nc.variables["runoff"][:].reshape(-1)[gid], a1[2])
+        assert same_bits(nc.variables["soil_water_layers"][:].reshape(-1, 8)[gid], a1[11:19].T)
