@@ -165,6 +165,38 @@ INTERFACE
     REAL(C_FLOAT), INTENT(OUT) :: lat (*)
     INTEGER(C_INT) :: h9g_land_cells
   END FUNCTION
+  ! NetCDF I/O (h9g_io.cpp): WRITE_NET_CDF_3DR.f90 / READ_PGF.f90
+  FUNCTION h9g_write_axy_nc (path, nx, ny, nlayers, zc, ncell, gid, annual) &
+      BIND(C, NAME='h9g_write_axy_nc')
+    IMPORT :: C_INT, C_CHAR, C_FLOAT, C_INT64_T
+    CHARACTER(KIND=C_CHAR), INTENT(IN) :: path (*)
+    INTEGER(C_INT), VALUE :: nx, ny, nlayers, ncell
+    REAL(C_FLOAT), INTENT(IN) :: zc (*), annual (*)
+    INTEGER(C_INT64_T), INTENT(IN) :: gid (*)
+    INTEGER(C_INT) :: h9g_write_axy_nc
+  END FUNCTION
+  FUNCTION h9g_nc_forcing_read (paths, nx, ny, ncell, gid, t0, nt, out) &
+      BIND(C, NAME='h9g_nc_forcing_read')
+    IMPORT :: C_INT, C_PTR, C_FLOAT, C_INT64_T
+    TYPE(C_PTR), INTENT(IN) :: paths (*)
+    INTEGER(C_INT), VALUE :: nx, ny, ncell, t0, nt
+    INTEGER(C_INT64_T), INTENT(IN) :: gid (*)
+    REAL(C_FLOAT) :: out (*)
+    INTEGER(C_INT) :: h9g_nc_forcing_read
+  END FUNCTION
+  FUNCTION h9g_nc_ntimes (path) BIND(C, NAME='h9g_nc_ntimes')
+    IMPORT :: C_INT, C_CHAR
+    CHARACTER(KIND=C_CHAR), INTENT(IN) :: path (*)
+    INTEGER(C_INT) :: h9g_nc_ntimes
+  END FUNCTION
+  FUNCTION h9g_nc_forcing_prefetch (ctx, slot, paths, nx, ny, t0, nt) &
+      BIND(C, NAME='h9g_nc_forcing_prefetch')
+    IMPORT :: C_INT, C_PTR
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT), VALUE :: slot, nx, ny, t0, nt
+    TYPE(C_PTR), INTENT(IN) :: paths (*)
+    INTEGER(C_INT) :: h9g_nc_forcing_prefetch
+  END FUNCTION
   FUNCTION h9g_last_kernel_ms (ctx) BIND(C, NAME='h9g_last_kernel_ms')
     IMPORT :: C_PTR, C_FLOAT
     TYPE(C_PTR), VALUE :: ctx

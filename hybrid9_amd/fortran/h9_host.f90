@@ -15,11 +15,19 @@ PROGRAM H9_HOST
 !   input_mode = 'case'  : a raw case directory (params.f32, forcing.f32,
 !                          optional state0.f32, case.nml) -- the same files
 !                          the reference harness oracle/_ref/h9ref reads
-! chosen in the optional namelist file h9gpu.nml (/h9gpu/).
+!   input_mode = 'pgf'   : forcing from the 7 PGF NetCDF files per decade
+!                          (READ_PGF.f90 names <var>_pgfv2.1_<syr>_<eyr>.nc4
+!                          in pgf_dir, netCDF classic), read on a host
+!                          thread and copied while the previous year runs
+!                          (h9g_nc_forcing_prefetch); synthetic soil
+! chosen in the optional namelist file h9gpu.nml (/h9gpu/); nx, ny, nland
+! override the synthetic grid.
 !
 ! Usage:  h9_host [driver.txt] [h9gpu.nml]
-! Outputs: <out_dir>/annual.f32 (ncell, 12+L, nyears) and
-!          <out_dir>/state_end.f32 (packed state, include/h9g.h).
+! Outputs: <out_dir>/annual.f32 (ncell, 12+L, nyears),
+!          <out_dir>/state_end.f32 (packed state, include/h9g.h) and, on a
+!          grid (synth/pgf), <PATH_output>/axyYYYY.nc per year as
+!          HYBRID9.f90:492-519 / WRITE_NET_CDF_3DR.f90 (nc_out = 1).
 !----------------------------------------------------------------------!
 USE, INTRINSIC :: ISO_C_BINDING
 USE H9_GPU
@@ -33,11 +41,17 @@ REAL :: lon_w, lat_w, lon_c_w, lat_c_w
 REAL(C_FLOAT) :: zi (0:H9G_LMAX+1)
 
 ! --- extension namelist ----------------------------------------------------
-CHARACTER (LEN = 512) :: input_mode, case_dir, out_dir
-INTEGER :: nlayers, grow_on, device, grid, year0, nyears
+CHARACTER (LEN = 512) :: input_mode, case_dir, out_dir, pgf_dir
+INTEGER :: nlayers, grow_on, device, grid, year0, nyears, nc_out, gnx, gny, gnland
 INTEGER(C_INT64_T) :: seed
 NAMELIST /h9gpu/ input_mode, case_dir, out_dir, nlayers, grow_on, device, &
-                 grid, year0, nyears, seed
+                 grid, year0, nyears, seed, pgf_dir, nc_out, gnx, gny, gnland
+CHARACTER (LEN = 600, KIND = C_CHAR), TARGET :: pgf_file (7)
+TYPE(C_PTR) :: pgf_ptr (7)
+CHARACTER (LEN = *), PARAMETER :: pgf_var (7) = &
+  (/ 'tas ', 'rlds', 'rsds', 'huss', 'ps  ', 'pr  ', 'rhs ' /)   ! READ_PGF.f90 order
+REAL(C_FLOAT) :: zc (H9G_LMAX)
+CHARACTER (LEN = 4) :: ydate
 
 ! --- case.nml of the harness (oracle/ref/h9ref_main.f90) -------------------
 INTEGER :: ncell, state_override, ntrace, trace_cells (64)
@@ -60,8 +74,10 @@ INTEGER :: time_BOY (2300-1860+1)
 !----------------------------------------------------------------------!
 ! Defaults, then driver.txt and h9gpu.nml.
 !----------------------------------------------------------------------!
-input_mode = 'synth'; case_dir = ''; out_dir = '.'
+input_mode = 'synth'; case_dir = ''; out_dir = '.'; pgf_dir = '.'
 nlayers = 8; grow_on = 1; device = 0; grid = 1; year0 = 0; nyears = 0
+nc_out = 1; gnx = 0; gny = 0; gnland = 0
+PATH_output = '.'
 seed = 20161123_C_INT64_T
 NISURF = 48; iDEC_start = 1; iDEC_end = 1
 zi = 0.0
@@ -131,9 +147,12 @@ ELSE
   ELSE
     nx = 1440; ny = 720; nland = 270000
   END IF
+  IF (gnx > 0) nx = gnx
+  IF (gny > 0) ny = gny
+  IF (gnland > 0) nland = gnland
   ncell = nland
   L = nlayers
-  IF (L == 10 .AND. grid == 1) STOP 'h9_host: L=10 uses the 0.25 deg grid'
+  IF (L == 10 .AND. grid == 1 .AND. gnx == 0) STOP 'h9_host: L=10 uses the 0.25 deg grid'
   IF (L == 10) zi (0:11) = (/ 0.0, 18.0, 45.0, 91.0, 166.0, 289.0, 493.0, &
                               829.0, 1383.0, 2296.0, 3500.0, 5000.0 /)
   ALLOCATE (gid (ncell), lat (ncell))
@@ -145,6 +164,11 @@ ELSE
     nyears = eyr - year0 + 1
   END IF
 END IF
+
+! layer centre depths for the output (INIT.f90:252-263, zc_o)
+DO i = 1, L
+  zc (i) = zi (i) - (zi (i) - zi (i-1)) / 2.0
+END DO
 
 !----------------------------------------------------------------------!
 ! GPU context.
@@ -199,6 +223,11 @@ DO iyr = 1, nyears
   CALL h9g_check_stop (ctx, rc)
   CALL chk (h9g_get_annual (ctx, annual))
   WRITE (u) annual
+  IF (nc_out /= 0 .AND. TRIM (input_mode) /= 'case') THEN     ! HYBRID9.f90:503-513
+    WRITE (ydate,'(I4)') jyear
+    CALL chk (h9g_write_axy_nc (TRIM (PATH_output)//'/axy'//ydate//'.nc'//C_NULL_CHAR, nx, ny, L, &
+                                zc, ncell, gid, annual))
+  END IF
   CALL chk (h9g_get_diagnostics (ctx, diag, C_NULL_PTR))
   WRITE (*,'(A,I5,A,I8,A,ES12.5,A,ES12.5,A,F9.1,A)') ' year', jyear, ' cells', NINT (diag (1)), &
         ' mean runoff', diag (2) / MAX (diag (1), 1.0D0), ' mm/s  mean soil water', &
@@ -226,9 +255,23 @@ CONTAINS
   SUBROUTINE stage (s, y, dfirst)
     INTEGER, INTENT(IN) :: s, y, dfirst
     INTEGER :: n
+    INTEGER :: idec, dsyr, deyr, k
+    CHARACTER (LEN = 9) :: decade
     n = time_BOY (y+1-1859) - time_BOY (y-1859)
     IF (TRIM (input_mode) == 'case') THEN
       CALL chk (h9g_push_forcing (ctx, s, n, forcing (:, dfirst:dfirst+n-1, :), 0))
+    ELSE IF (TRIM (input_mode) == 'pgf') THEN
+      ! decade files of READ_PGF.f90:22-106; day index within the file
+      idec = (y - 1901) / 10 + 1
+      dsyr = (idec - 1) * 10 + 1901
+      deyr = MERGE (dsyr + 9, dsyr + 1, idec < 12)
+      WRITE (decade,'(I4,A,I4)') dsyr, '_', deyr
+      DO k = 1, 7
+        pgf_file (k) = TRIM (pgf_dir)//'/'//TRIM (pgf_var (k))//'_pgfv2.1_'//decade//'.nc4'//C_NULL_CHAR
+        pgf_ptr (k) = C_LOC (pgf_file (k))
+      END DO
+      CALL chk (h9g_nc_forcing_prefetch (ctx, s, pgf_ptr, nx, ny, &
+                                         time_BOY (y-1859) - time_BOY (dsyr-1859), n))
     ELSE
       CALL chk (h9g_synth_forcing (ctx, s, seed, time_BOY (y-1859) - time_BOY (1901-1859), n))
     END IF

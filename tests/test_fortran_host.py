@@ -73,3 +73,55 @@ def test_fortran_host_matches_reference_golden(tmp_path, name):
     st = np.fromfile(tmp_path / "state_end.f32", np.float32)
     assert same_bits(ann, exp["annual"])
     assert same_bits(st, exp["state"])
+
+
+@pytest.mark.gpu
+def test_fortran_host_pgf_netcdf_mode(tmp_path):
+    """The Fortran host's PGF path: forcing from decade NetCDF files named as
+    READ_PGF.f90:22-106 (async prefetch), annual output as axyYYYY.nc
+    (HYBRID9.f90:503-513, WRITE_NET_CDF_3DR.f90); equal to the Python mirror
+    fed the same forcing."""
+    from scipy.io import netcdf_file
+    from hybrid9_amd import synth
+    from tests.test_netcdf import write_pgf_like
+    exe = _build()
+    nx, ny, nland = 20, 10, 48
+    gid = synth.land_cells(nx, ny, nland)
+    lat = synth.cell_lat(gid, nx, ny)
+    nt = sum(synth.days_in_year(1901 + k) for k in range(10))
+    f = synth.make_forcing(gid, lat, 0, 366 + 365)          # the first two years suffice
+    full = np.full((7, nt, ny * nx), np.float32(280.0))
+    full[:, :f.shape[1]][:, :, gid] = f
+    pgf = tmp_path / "pgf"
+    pgf.mkdir()
+    for k, v in enumerate(h.PGF_VARS):
+        p = write_pgf_like(pgf, v, full[k].reshape(nt, ny, nx), 2)
+        p.rename(pgf / f"{v}_pgfv2.1_1901_1910.nc4")
+    out = tmp_path / "out"
+    out.mkdir()
+    drv = tmp_path / "driver.txt"
+    drv.write_text(f"'{out}'\n48\n.T.\n 1\n 1\n.F.\n .F.\n 'a'\n 'b'\n 1901\n 1902\n 0\n0.0\n0.0\n 1\n 1\n" +
+                   "".join(f"{v}\n" for v in synth.ZI_L8[:10]))
+    nml = tmp_path / "h9gpu.nml"
+    nml.write_text(f"&h9gpu\n input_mode='pgf', pgf_dir='{pgf}', out_dir='{tmp_path}', grow_on=1,\n"
+                   f" year0=1901, nyears=2, gnx={nx}, gny={ny}, gnland={nland}\n/\n")
+    r = subprocess.run([str(exe), str(drv), str(nml)], capture_output=True, text=True, timeout=600)
+    assert "completed successfully" in r.stdout, r.stdout + r.stderr
+    ann = np.fromfile(tmp_path / "annual.f32", np.float32).reshape(2, 20, nland)
+    with h.Context(nland, synth.ZI_L8, nisurf=48) as ctx:      # the Python mirror, same inputs
+        ctx.set_cells(gid, lat)
+        ctx.synth_params(synth.SEED)
+        ctx.init_state()
+        ctx.push_forcing(0, f[:, :365])
+        ctx.run_year(0, 1901)
+        ctx.sync()
+        a0 = ctx.get_annual()
+        ctx.push_forcing(1, f[:, 365:365 + 365])
+        ctx.run_year(1, 1902)
+        ctx.sync()
+        a1 = ctx.get_annual()
+    assert same_bits(ann[0], a0) and same_bits(ann[1], a1)
+    for y, a in ((1901, a0), (1902, a1)):
+        with netcdf_file(out / f"axy{y}.nc", "r", mmap=False) as nc:
+            assert same_bits(nc.variables["runoff"][:].reshape(-1)[gid], a[2])
+            assert same_bits(nc.variables["soil_water"][:].reshape(-1)[gid], a[19])
