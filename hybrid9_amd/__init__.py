@@ -118,6 +118,11 @@ def lib() -> C.CDLL:
         "h9g_nc_ntimes": (C.c_int, [C.c_char_p]),
         "h9g_nc_forcing_prefetch": (C.c_int, [vp, C.c_int, C.POINTER(C.c_char_p), C.c_int, C.c_int,
                                               C.c_int, C.c_int]),
+        "h9g_soil_layer": (C.c_int, [vp, C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int]),
+        "h9g_soil_fmax": (C.c_int, [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int, C.c_int]),
+        "h9g_last_soil_ms": (C.c_float, [vp]),
+        "h9g_last_soil_slow": (C.c_int, [vp]),
+        "h9g_get_params": (C.c_int, [vp, _FP, _FP, _FP, _FP, _FP]),
         "h9g_host_expf": (C.c_float, [C.c_float]),
         "h9g_host_powf": (C.c_float, [C.c_float, C.c_float]),
     }
@@ -215,6 +220,36 @@ class Context:
             assert a.shape == (self.ncell, self.L), a.shape
         assert arrs[4].shape == (self.ncell,)
         _check(self._lib.h9g_set_params(self._h, *[_fp(a) for a in arrs]), "h9g_set_params")
+
+    def get_params(self) -> dict:
+        out = {k: np.empty((self.ncell, self.L), np.float32) for k in ("theta_s", "hksat", "bsw", "psi_s")}
+        out["fmax"] = np.empty(self.ncell, np.float32)
+        _check(self._lib.h9g_get_params(self._h, *[_fp(out[k]) for k in
+                                                   ("theta_s", "hksat", "bsw", "psi_s", "fmax")]),
+               "h9g_get_params")
+        return out
+
+    def soil_layer(self, layer: int, ts, ks, lm, ps, nx: int, ny: int):
+        """INIT.f90:575-631 for one layer: 30" fields as (ny*60, nx*60) float32
+        host arrays, or device pointers (ints, e.g. tensor.data_ptr())."""
+        if all(isinstance(a, int) for a in (ts, ks, lm, ps)):
+            ptrs, dev = [C.c_void_p(a) for a in (ts, ks, lm, ps)], 1
+        else:
+            arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (ts, ks, lm, ps)]
+            for a in arrs:
+                assert a.shape == (ny * 60, nx * 60), a.shape
+            ptrs, dev = [a.ctypes.data_as(C.c_void_p) for a in arrs], 0
+        _check(self._lib.h9g_soil_layer(self._h, layer, *ptrs, nx, ny, dev), "h9g_soil_layer")
+        return float(self._lib.h9g_last_soil_ms(self._h)), int(self._lib.h9g_last_soil_slow(self._h))
+
+    def soil_fmax(self, soil_tex, fmax, nx: int, ny: int):
+        """INIT.f90:661-680 (0.5 deg integer grids (ny, nx)); completes the parameters."""
+        t = np.ascontiguousarray(soil_tex, dtype=np.int32)
+        f = np.ascontiguousarray(fmax, dtype=np.int32)
+        assert t.size == f.size == nx * ny
+        i32 = C.POINTER(C.c_int32)
+        _check(self._lib.h9g_soil_fmax(self._h, t.ctypes.data_as(i32), f.ctypes.data_as(i32), nx, ny),
+               "h9g_soil_fmax")
 
     def init_state(self):
         _check(self._lib.h9g_init_state(self._h), "h9g_init_state")

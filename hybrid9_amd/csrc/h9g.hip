@@ -375,6 +375,114 @@ __global__ void __launch_bounds__(H9G_BLOCK) h9g_synth_forcing_kernel(int ncell,
   for (int k = 0; k < 7; k++) forc[k * fvar + (size_t)d * ncell + c] = v[k];
 }
 
+// ---------------------------------------------------------------------------
+// Soil parameter build, INIT.f90:575-631: each 0.5 deg
+// cell of the context averages its 60x60 block of 30" pixels whose
+// theta_s >= 0, then converts units.  The reference sums sequentially
+// (x1 outer, y1 inner).  h9g_soil_kernel reads the block coalesced (a wave
+// per pixel row) and reduces in a tree; that equals the sequential sum
+// bit for bit whenever every contributing value is an integer of
+// magnitude <= 4096 (the BNU fields are stored as scaled integers): all
+// partial sums are then exact floats below 2^24.  Any other block is
+// flagged and summed in the reference's order by h9g_soil_seq_kernel.
+// ---------------------------------------------------------------------------
+#define H9G_SWAVES 4
+struct SoilOut {
+  __device__ __forceinline__ static void store(float *par, int L, int layer, size_t n, int c, int v,
+                                                float sum, int j) {
+    float m = sum;
+    if (j > 0) m = m / (float)j;                                  // INIT.f90:593-598
+    float out;
+    if (v == 0) out = m / 1.0E3f;                                 // theta_s      :613
+    else if (v == 1) out = 10.0f * m / 86400.0f;                  // hksat        :614
+    else if (v == 2) out = 1.0f / MAXF(m / 1.0E3f, 1.0E-8f);      // bsw          :615,624,628
+    else out = 10.0f * m;                                         // psi_s        :616
+    par[(size_t)(v * L + layer) * n + c] = out;
+  }
+};
+
+__device__ __forceinline__ bool small_int(float v) { return v == __builtin_truncf(v) && __builtin_fabsf(v) <= 4096.0f; }
+
+__global__ void __launch_bounds__(64 * H9G_SWAVES) h9g_soil_kernel(int nx, int ncell, const int64_t *__restrict__ gid,
+                                                                  const float *__restrict__ ts,
+                                                                  const float *__restrict__ ks,
+                                                                  const float *__restrict__ lm,
+                                                                  const float *__restrict__ ps, size_t pitch, int L,
+                                                                  int layer, float *__restrict__ par,
+                                                                  int *__restrict__ slow) {
+  __shared__ float red[H9G_SWAVES][5];
+  __shared__ int red_ok[H9G_SWAVES];
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t g = gid[c];
+  const int x = (int)(g % nx), y = (int)(g / nx);
+  const size_t base = (size_t)y * 60 * pitch + (size_t)x * 60 + lane;
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f, sj = 0.0f;
+  bool ok = true;
+  if (lane < 60) {
+#pragma unroll 5
+    for (int r = wave; r < 60; r += H9G_SWAVES) {                 // one pixel row per wave
+      const size_t i = base + (size_t)r * pitch;
+      const float a = ts[i];
+      if (a >= 0.0f) {                                            // :584
+        const float b = ks[i], d = lm[i], e = ps[i];
+        s0 += a; s1 += b; s2 += d; s3 += e; sj += 1.0f;
+        ok = ok && small_int(a) && small_int(b) && small_int(d) && small_int(e);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {                              // wave tree (exact: see above)
+    s0 += __shfl_xor(s0, o); s1 += __shfl_xor(s1, o); s2 += __shfl_xor(s2, o);
+    s3 += __shfl_xor(s3, o); sj += __shfl_xor(sj, o);
+  }
+  const bool wok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+  if (lane == 0) {
+    red[wave][0] = s0; red[wave][1] = s1; red[wave][2] = s2; red[wave][3] = s3; red[wave][4] = sj;
+    red_ok[wave] = wok;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int v = threadIdx.x;
+    bool all = true;
+    float sum = 0.0f, cnt = 0.0f;
+    for (int w = 0; w < H9G_SWAVES; w++) {
+      all = all && red_ok[w];
+      sum += red[w][v];
+      cnt += red[w][4];
+    }
+    if (!all) {
+      if (v == 0) slow[c] = 1;
+    } else {
+      SoilOut::store(par, L, layer, (size_t)ncell, c, v, sum, (int)cnt);
+    }
+  }
+}
+
+// The reference's order for the flagged blocks: thread (cell, variable).
+__global__ void h9g_soil_seq_kernel(int nx, int ncell, const int64_t *__restrict__ gid, const float *__restrict__ ts,
+                                    const float *__restrict__ ks, const float *__restrict__ lm,
+                                    const float *__restrict__ ps, size_t pitch, int L, int layer,
+                                    float *__restrict__ par, const int *__restrict__ slow) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = t >> 2, v = t & 3;
+  if (c >= ncell || !slow[c]) return;
+  const float *src = v == 0 ? ts : (v == 1 ? ks : (v == 2 ? lm : ps));
+  const int64_t g = gid[c];
+  const int x = (int)(g % nx), y = (int)(g / nx);
+  float sum = 0.0f;
+  int j = 0;
+  for (int x1 = x * 60; x1 < x * 60 + 60; x1++)                  // :582-592, x1 outer
+    for (int y1 = y * 60; y1 < y * 60 + 60; y1++) {
+      const size_t i = (size_t)y1 * pitch + x1;
+      if (ts[i] >= 0.0f) {
+        sum = sum + src[i];
+        j = j + 1;
+      }
+    }
+  SoilOut::store(par, L, layer, (size_t)ncell, c, v, sum, j);
+}
+
 // MathFast's division path with a device-computed reciprocal (recip64).
 __global__ void h9g_div_kernel(int n, const float *x, const float *d, float *out, int *flag) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -423,6 +531,10 @@ struct h9g_ctx {
   std::vector<float *> h_pin;     // per-slot pinned staging of the NetCDF prefetch
   std::vector<std::thread> prefetch;
   std::vector<int> prefetch_rc;
+  unsigned soil_layers = 0;       // layers built by h9g_soil_layer (bit i = layer i)
+  float soil_ms = 0.0f;           // device time of the last h9g_soil_layer
+  int soil_slow = 0;              // cells of the last layer summed in the reference's order
+  int *d_slow = nullptr;
   int kind = 1;        // 1: h9g_pair_kernel (default), 2: h9g_solo_kernel (H9G_KERNEL=solo)
 };
 
@@ -510,6 +622,7 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_gid);
   (void)hipFree(ctx->d_lat);
   (void)hipFree(ctx->d_stamps);
+  (void)hipFree(ctx->d_slow);
   for (auto e : ctx->ev_copied) hipEventDestroy(e);
   for (auto e : ctx->ev_consumed) hipEventDestroy(e);
   for (int i = 0; i < NEVT; i++) {
@@ -598,6 +711,23 @@ int h9g_set_params(h9g_ctx *ctx, const float *theta_s, const float *hksat, const
   HIPCHK(hipMemcpyAsync(ctx->d_par, rows.data(), sizeof(float) * rows.size(), hipMemcpyHostToDevice, ctx->sc));
   HIPCHK(hipStreamSynchronize(ctx->sc));
   ctx->params_set = 1;
+  return 0;
+}
+
+// device rows -> (L, ncell) layer-fastest host arrays (h9g_set_params layout)
+int h9g_get_params(h9g_ctx *ctx, float *theta_s, float *hksat, float *bsw, float *psi_s, float *fmax) {
+  if (!ctx || !theta_s || !hksat || !bsw || !psi_s || !fmax) return H9G_EINVAL;
+  const size_t n = ctx->n;
+  const int L = ctx->L;
+  std::vector<float> rows((4 * L + 1) * n);
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  HIPCHK(hipMemcpy(rows.data(), ctx->d_par, sizeof(float) * rows.size(), hipMemcpyDeviceToHost));
+  float *dst[4] = {theta_s, hksat, bsw, psi_s};
+  for (int k = 0; k < 4; k++)
+    for (size_t c = 0; c < n; c++)
+      for (int i = 0; i < L; i++) dst[k][c * L + i] = rows[(size_t)(k * L + i) * n + c];
+  memcpy(fmax, &rows[(size_t)(4 * L) * n], sizeof(float) * n);
   return 0;
 }
 
@@ -906,6 +1036,92 @@ int h9g_nc_forcing_prefetch(h9g_ctx *ctx, int slot, const char *const *paths, in
   });
   return 0;
 }
+
+// INIT.f90:575-631 for one soil layer (0-based) of the context's cells
+// (h9g_set_cells).  ts, ks, lm, ps: the layer's 30" fields, (ny*60) rows of
+// nx*60 values (row 0 north), device pointers if on_device else host
+// (copied through a device staging buffer).  Writes the theta_s, hksat,
+// bsw, psi_s rows of the parameters.
+int h9g_soil_layer(h9g_ctx *ctx, int layer, const float *ts, const float *ks, const float *lm, const float *ps,
+                   int nx, int ny, int on_device) {
+  if (!ctx || layer < 0 || layer >= ctx->L || !ts || !ks || !lm || !ps || nx <= 0 || ny <= 0) return H9G_EINVAL;
+  if (ctx->h_gid.size() != ctx->n) return H9G_ESTATE;
+  for (auto g : ctx->h_gid)
+    if (g < 0 || g >= (int64_t)nx * ny) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  const size_t pitch = (size_t)nx * 60, npix = pitch * (size_t)ny * 60;
+  const float *src[4] = {ts, ks, lm, ps};
+  float *stage = nullptr;
+  if (!on_device) {
+    HIPCHK(hipMalloc(&stage, sizeof(float) * 4 * npix));
+    for (int k = 0; k < 4; k++) {
+      HIPCHK(hipMemcpyAsync(stage + k * npix, src[k], sizeof(float) * npix, hipMemcpyHostToDevice, ctx->sc));
+      src[k] = stage + k * npix;
+    }
+  }
+  if (!ctx->d_slow) HIPCHK(hipMalloc(&ctx->d_slow, sizeof(int) * ctx->n));
+  HIPCHK(hipMemsetAsync(ctx->d_slow, 0, sizeof(int) * ctx->n, ctx->sc));
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, ctx->sc));
+  const int n = (int)ctx->n;
+  h9g_soil_kernel<<<n, 64 * H9G_SWAVES, 0, ctx->sc>>>(nx, n, ctx->d_gid, src[0], src[1], src[2], src[3], pitch,
+                                                      ctx->L, layer, ctx->d_par, ctx->d_slow);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e1, ctx->sc));
+  h9g_soil_seq_kernel<<<(4 * n + 255) / 256, 256, 0, ctx->sc>>>(nx, n, ctx->d_gid, src[0], src[1], src[2], src[3],
+                                                               pitch, ctx->L, layer, ctx->d_par, ctx->d_slow);
+  HIPCHK(hipGetLastError());
+  std::vector<int> slow(ctx->n);
+  HIPCHK(hipMemcpyAsync(slow.data(), ctx->d_slow, sizeof(int) * ctx->n, hipMemcpyDeviceToHost, ctx->sc));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  HIPCHK(hipEventElapsedTime(&ctx->soil_ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (stage) HIPCHK(hipFree(stage));
+  ctx->soil_slow = 0;
+  for (int v : slow) ctx->soil_slow += v != 0;
+  ctx->soil_layers |= 1u << layer;
+  return 0;
+}
+
+// INIT.f90:661-680 after every layer is built: Fmax of the soiled cells
+// (soil_tex > 0, /= 13, SUM(theta_s) > trunc) from the 0.5 deg integer field
+// (-9999 -> 3809), NaN elsewhere.  soil_tex, fmax: host (ny, nx) grids.
+// The parameters are then complete (h9g_init_state may follow).
+int h9g_soil_fmax(h9g_ctx *ctx, const int32_t *soil_tex, const int32_t *fmax, int nx, int ny) {
+  if (!ctx || !soil_tex || !fmax || nx <= 0 || ny <= 0) return H9G_EINVAL;
+  if (ctx->h_gid.size() != ctx->n || ctx->soil_layers != (1u << ctx->L) - 1) return H9G_ESTATE;
+  const size_t n = ctx->n;
+  const int L = ctx->L;
+  HIPCHK(hipSetDevice(ctx->device));
+  std::vector<float> ts((size_t)L * n), fm(n);
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  HIPCHK(hipMemcpy(ts.data(), ctx->d_par, sizeof(float) * L * n, hipMemcpyDeviceToHost));
+  for (size_t c = 0; c < n; c++) {
+    const int64_t g = ctx->h_gid[c];
+    if (g < 0 || g >= (int64_t)nx * ny) return H9G_EINVAL;
+    float sum = 0.0f;
+    for (int i = 0; i < L; i++) sum = sum + ts[(size_t)i * n + c];
+    const int tex = soil_tex[g];
+    if (tex > 0 && tex != 13 && sum > 1.0E-8f) {
+      int v = fmax[g];
+      if (v == -9999) v = 3809;
+      fm[c] = (float)v / 10000.0f;
+    } else {
+      fm[c] = __builtin_nanf("");
+    }
+  }
+  HIPCHK(hipMemcpy(ctx->d_par + (size_t)(4 * L) * n, fm.data(), sizeof(float) * n, hipMemcpyHostToDevice));
+  ctx->params_set = 1;
+  return 0;
+}
+
+// Device time of the last h9g_soil_layer's block-average kernel, and the
+// number of its cells that took the reference-order path.
+float h9g_last_soil_ms(h9g_ctx *ctx) { return ctx ? ctx->soil_ms : 0.0f; }
+int h9g_last_soil_slow(h9g_ctx *ctx) { return ctx ? ctx->soil_slow : -1; }
 
 float h9g_last_kernel_ms(h9g_ctx *ctx) { return ctx ? ctx->last_ms : 0.0f; }
 

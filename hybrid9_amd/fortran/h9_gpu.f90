@@ -197,6 +197,38 @@ INTERFACE
     TYPE(C_PTR), INTENT(IN) :: paths (*)
     INTEGER(C_INT) :: h9g_nc_forcing_prefetch
   END FUNCTION
+  ! soil parameter build (INIT.f90:492-680)
+  FUNCTION h9g_soil_layer (ctx, layer, ts, ks, lm, ps, nx, ny, on_device) &
+      BIND(C, NAME='h9g_soil_layer')
+    IMPORT :: C_INT, C_PTR, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT), VALUE :: layer, nx, ny, on_device
+    REAL(C_FLOAT), INTENT(IN) :: ts (*), ks (*), lm (*), ps (*)
+    INTEGER(C_INT) :: h9g_soil_layer
+  END FUNCTION
+  FUNCTION h9g_soil_fmax (ctx, soil_tex, fmax, nx, ny) BIND(C, NAME='h9g_soil_fmax')
+    IMPORT :: C_INT, C_PTR, C_INT32_T
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT32_T), INTENT(IN) :: soil_tex (*), fmax (*)
+    INTEGER(C_INT), VALUE :: nx, ny
+    INTEGER(C_INT) :: h9g_soil_fmax
+  END FUNCTION
+  FUNCTION h9g_last_soil_ms (ctx) BIND(C, NAME='h9g_last_soil_ms')
+    IMPORT :: C_PTR, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    REAL(C_FLOAT) :: h9g_last_soil_ms
+  END FUNCTION
+  FUNCTION h9g_last_soil_slow (ctx) BIND(C, NAME='h9g_last_soil_slow')
+    IMPORT :: C_PTR, C_INT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT) :: h9g_last_soil_slow
+  END FUNCTION
+  FUNCTION h9g_get_params (ctx, theta_s, hksat, bsw, psi_s, fmax) BIND(C, NAME='h9g_get_params')
+    IMPORT :: C_INT, C_PTR, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    REAL(C_FLOAT) :: theta_s (*), hksat (*), bsw (*), psi_s (*), fmax (*)
+    INTEGER(C_INT) :: h9g_get_params
+  END FUNCTION
   FUNCTION h9g_last_kernel_ms (ctx) BIND(C, NAME='h9g_last_kernel_ms')
     IMPORT :: C_PTR, C_FLOAT
     TYPE(C_PTR), VALUE :: ctx

@@ -162,6 +162,28 @@ int h9g_nc_ntimes(const char *path);
 int h9g_nc_forcing_prefetch(h9g_ctx *ctx, int slot, const char *const *paths,
                             int nx, int ny, int t0, int nt);
 
+/* --- soil parameter build (INIT.f90:492-680) --------------------------- */
+/* One soil layer (0-based) of the context's cells (h9g_set_cells): the
+ * 60x60 block average of the layer's 30" fields theta_s (0.001 cm3/cm3),
+ * k_s (cm/day), lambda (0.001), psi_s (cm) over pixels with theta_s >= 0,
+ * and the unit conversions of INIT.f90:611-628.  Fields: (ny*60) rows of
+ * nx*60 floats, row 0 north; device pointers if on_device, else host. */
+int h9g_soil_layer(h9g_ctx *ctx, int layer, const float *ts, const float *ks,
+                   const float *lm, const float *ps, int nx, int ny,
+                   int on_device);
+/* INIT.f90:661-680 once all layers are built: Fmax of the soiled cells
+ * from the 0.5 deg integer grids soil_tex and fmax (ny, nx); completes the
+ * parameters (replaces h9g_set_params). */
+int h9g_soil_fmax(h9g_ctx *ctx, const int32_t *soil_tex, const int32_t *fmax,
+                  int nx, int ny);
+/* Device ms of the last soil layer's block-average kernel; number of its
+ * cells summed in the reference's sequential order (non-integer data). */
+float h9g_last_soil_ms(h9g_ctx *ctx);
+int h9g_last_soil_slow(h9g_ctx *ctx);
+/* Parameters back to the host, h9g_set_params layouts. */
+int h9g_get_params(h9g_ctx *ctx, float *theta_s, float *hksat, float *bsw,
+                   float *psi_s, float *fmax);
+
 /* --- measurement ------------------------------------------------------ */
 /* Device time (HIP events on the compute stream) of the last year kernel,
  * and of all year kernels since the last reset. */

@@ -776,3 +776,67 @@ int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
   if (err) *err = first;
   return first_code;
 }
+
+/* ----------------------------------------------------------------------
+ * Soil parameter build, INIT.f90:575-631 (one soil layer) and :661-680
+ * (Fmax), for the 0.5-degree cells gid (iy*nx+ix, row iy from the north).
+ * Input fields are the 30" layers as read at INIT.f90:540-569: ny*60 rows
+ * of nx*60 values, row-major (the Fortran (x1,y1) with x1 fastest).
+ * Parity unpinned against the reference itself (INIT.f90 needs the
+ * netCDF-Fortran library, absent here); tests/test_soil.py pins this
+ * restatement with an independent numpy loop.
+ * -------------------------------------------------------------------- */
+void h9o_soil_layer(int nx, int ny, int ncell, const int64_t *gid, const float *ts_in,
+                    const float *ks_in, const float *lm_in, const float *ps_in, float *theta_s,
+                    float *hksat, float *bsw, float *psi_s) {
+  const float zero = 0.0f, trunc = 1.0E-8f;     /* SHARED.f90:506 */
+  const size_t W = (size_t)nx * 60;
+  (void)ny;
+  for (int c = 0; c < ncell; c++) {
+    const int x = (int)(gid[c] % nx), y = (int)(gid[c] / nx);
+    float ts = zero, ks = zero, lm = zero, ps = zero;   /* :575-578 */
+    int j = 0;
+    for (int x1 = x * 60; x1 < x * 60 + 60; x1++)       /* :582-592, x1 outer */
+      for (int y1 = y * 60; y1 < y * 60 + 60; y1++) {
+        const size_t k = (size_t)y1 * W + x1;
+        if (ts_in[k] >= zero) {
+          ts = ts + ts_in[k];
+          ks = ks + ks_in[k];
+          lm = lm + lm_in[k];
+          ps = ps + ps_in[k];
+          j = j + 1;
+        }
+      }
+    if (j > 0) {                                         /* :593-598 */
+      ts = ts / (float)j;
+      ks = ks / (float)j;
+      lm = lm / (float)j;
+      ps = ps / (float)j;
+    }
+    theta_s[c] = ts / 1.0E3f;                            /* :613-628 */
+    hksat[c] = 10.0f * ks / 86400.0f;
+    float lambda = lm / 1.0E3f;
+    psi_s[c] = 10.0f * ps;
+    lambda = MAXF(lambda, trunc);
+    bsw[c] = 1.0f / lambda;
+  }
+}
+
+/* INIT.f90:661-680: Fmax of soiled cells from the 0.5-degree integer field
+ * (missing -9999 -> global mean 3809), NaN elsewhere.  theta_s (ncell, L). */
+void h9o_soil_fmax(int ncell, int L, const int64_t *gid, const int32_t *soil_tex,
+                   const int32_t *fmax_in, const float *theta_s, float *fmax) {
+  const float trunc = 1.0E-8f;
+  for (int c = 0; c < ncell; c++) {
+    float sum = 0.0f;
+    for (int i = 0; i < L; i++) sum = sum + theta_s[(size_t)c * L + i];
+    const int tex = soil_tex[gid[c]];
+    if (tex > 0 && tex != 13 && sum > trunc) {
+      int v = fmax_in[gid[c]];
+      if (v == -9999) v = 3809;
+      fmax[c] = (float)v / 10000.0f;
+    } else {
+      fmax[c] = NAN;
+    }
+  }
+}

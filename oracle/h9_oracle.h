@@ -19,6 +19,7 @@
  * Layouts: see oracle/refcase.py.  L <= H9O_LMAX soil layers.
  */
 #ifndef H9_ORACLE_H
+#include <stdint.h>
 #define H9_ORACLE_H
 
 #ifdef __cplusplus
@@ -61,6 +62,13 @@ int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
             const float *zi, const float *params, const float *forcing,
             float *state, float *annual, int ntrace, const int *trace_cells,
             float *trace, int nthreads, h9o_error *err);
+
+/* Soil parameter build (INIT.f90:575-631 one layer, :661-680 Fmax). */
+void h9o_soil_layer(int nx, int ny, int ncell, const int64_t *gid, const float *ts_in,
+                    const float *ks_in, const float *lm_in, const float *ps_in, float *theta_s,
+                    float *hksat, float *bsw, float *psi_s);
+void h9o_soil_fmax(int ncell, int L, const int64_t *gid, const int32_t *soil_tex,
+                   const int32_t *fmax_in, const float *theta_s, float *fmax);
 
 #ifdef __cplusplus
 }

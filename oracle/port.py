@@ -40,6 +40,10 @@ def lib():
         _lib.h9o_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  f, f, f, f, f, C.c_int, C.POINTER(C.c_int), f,
                                  C.c_int, C.POINTER(H9OError)]
+        i64 = C.POINTER(C.c_int64)
+        _lib.h9o_soil_layer.argtypes = [C.c_int, C.c_int, C.c_int, i64, f, f, f, f, f, f, f, f]
+        _lib.h9o_soil_fmax.argtypes = [C.c_int, C.c_int, i64, C.POINTER(C.c_int32),
+                                       C.POINTER(C.c_int32), f, f]
     return _lib
 
 
@@ -75,7 +79,7 @@ def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=1,
         st = init_state(params, zi)
     else:
         st = refcase.pack_state(state0, L)
-    ann = np.zeros((nyears, 12 + L, n), dtype=np.float32)
+    ann = np.full((nyears, 12 + L, n), np.nan, dtype=np.float32)   # non-soil cells stay NaN (INIT.f90:402-414)
     ndays = fo.shape[1]
     tc = np.asarray(sorted(trace_cells), dtype=np.int32)
     tr = np.zeros((max(len(tc), 1), ndays * nisurf, refcase.trace_width(L)), dtype=np.float32)
@@ -88,4 +92,28 @@ def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=1,
                         value=err.value))
     if len(tc):
         out["trace"] = tr
+    return out
+
+
+def soil_layer(nx, ny, gid, ts, ks, lm, ps):
+    """INIT.f90:575-631 restated (h9o_soil_layer): returns theta_s, hksat,
+    bsw, psi_s of one layer for the cells gid."""
+    gid = np.ascontiguousarray(gid, np.int64)
+    a = [np.ascontiguousarray(x, np.float32) for x in (ts, ks, lm, ps)]
+    out = [np.empty(gid.size, np.float32) for _ in range(4)]
+    lib().h9o_soil_layer(nx, ny, gid.size, gid.ctypes.data_as(C.POINTER(C.c_int64)),
+                         *[_fp(x) for x in a], *[_fp(o) for o in out])
+    return out
+
+
+def soil_fmax(gid, soil_tex, fmax_in, theta_s):
+    """INIT.f90:661-680 restated (h9o_soil_fmax); theta_s (ncell, L)."""
+    gid = np.ascontiguousarray(gid, np.int64)
+    t = np.ascontiguousarray(soil_tex, np.int32).reshape(-1)
+    fm = np.ascontiguousarray(fmax_in, np.int32).reshape(-1)
+    ts = np.ascontiguousarray(theta_s, np.float32)
+    out = np.empty(gid.size, np.float32)
+    i32 = C.POINTER(C.c_int32)
+    lib().h9o_soil_fmax(gid.size, ts.shape[1], gid.ctypes.data_as(C.POINTER(C.c_int64)),
+                        t.ctypes.data_as(i32), fm.ctypes.data_as(i32), _fp(ts), _fp(out))
     return out
