@@ -133,16 +133,20 @@ def cpu_baseline(workload: dict, seed: int) -> dict:
                       f"{'' if ok else ' (a sample process STOPped)'}"}
 
 
-def load_traffic(workload_name: str):
-    """HBM traffic per launch measured with rocprofv3 PMC counters
-    (profiles/pmc_*.json, written by tools/pmc_traffic.py)."""
+def load_traffic(workload_name: str, kernel: str):
+    """HBM traffic per launch of this kernel, measured with rocprofv3 PMC
+    counters (profiles/pmc_<tag>.json, tools/prof.sh + tools/pmc_summary.py):
+    the latest-tagged summary of the same workload and kernel instantiation."""
+    def norm(k):
+        k = k.replace("void ", "").replace("h9k::", "").replace(" ", "")
+        return k.split("(")[0]
     best = None
-    for p in sorted((ROOT / "profiles").glob("pmc_*.json")):
+    for p in sorted((ROOT / "profiles").glob("pmc_*.json")):     # tags sort by round/version
         try:
             d = json.loads(p.read_text())
         except Exception:
             continue
-        if d.get("workload") == workload_name:
+        if d.get("workload") == workload_name and norm(d.get("kernel", "")) == norm(kernel):
             best = d
     return best
 
@@ -218,7 +222,7 @@ def main():
     launch_s = kern_ms / 1e3 / K
     algo_bytes_launch = cell_steps_rank / K * bytes_per_cell_step(L)
     achieved = algo_bytes_launch / launch_s / 1e9
-    pmc = load_traffic(args.workload)
+    pmc = load_traffic(args.workload, ctx.kernel_name())
     traffic = None
     if pmc and pmc.get("hbm_bytes_per_launch"):
         traffic = pmc["hbm_bytes_per_launch"] / launch_s / 1e9
