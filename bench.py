@@ -80,7 +80,9 @@ def dist_setup(n_gpus: int):
 
 
 def barrier_sync(ctx, torch, dist, world):
-    ctx.sync()
+    # a cell reaching one of the reference's STOPs (synthetic L=10 cells can)
+    # is marked failed and NaN, as the error record says; the others go on
+    ctx.sync(raise_on_stop=False)
     if torch is not None and torch.cuda.is_available():
         torch.cuda.synchronize()
     if world > 1:
@@ -217,8 +219,12 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
         diag = diag_t.cpu().numpy()
 
-    cell_steps_rank = sum(gid.size * synth.days_in_year(y) * ns for y in years[W:])
-    value = world * cell_steps_rank / elapsed
+    # cells that hit a reference STOP stop computing: count only the others
+    # (diag is the all-reduced sum over ranks for N > 1)
+    failed = int(round(float(diag[11]))) if diag is not None else 0
+    steps_per_cell = sum(synth.days_in_year(y) * ns for y in years[W:])
+    cell_steps_rank = (gid.size - failed / world) * steps_per_cell
+    value = (world * gid.size - failed) * steps_per_cell / elapsed
     launch_s = kern_ms / 1e3 / K
     algo_bytes_launch = cell_steps_rank / K * bytes_per_cell_step(L)
     achieved = algo_bytes_launch / launch_s / 1e9
@@ -252,6 +258,7 @@ def main():
                      "traffic_source": (pmc or {}).get("source")},
         "cpu_baseline": None,
         "diagnostics_last_year": {k: float(v) for k, v in zip(h.DIAG_NAMES, diag)},
+        "cells_stopped": failed,
     }
     ctx.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
