@@ -123,6 +123,7 @@ def lib() -> C.CDLL:
         "h9g_last_soil_ms": (C.c_float, [vp]),
         "h9g_last_soil_slow": (C.c_int, [vp]),
         "h9g_get_params": (C.c_int, [vp, _FP, _FP, _FP, _FP, _FP]),
+        "h9g_run_site": (C.c_int, [vp, C.c_int, _FP, _FP, _FP, _FP]),
         "h9g_host_expf": (C.c_float, [C.c_float]),
         "h9g_host_powf": (C.c_float, [C.c_float, C.c_float]),
     }
@@ -300,6 +301,29 @@ class Context:
     # -- hot path ---------------------------------------------------------
     def run_year(self, slot: int, jyear: int):
         _check(self._lib.h9g_run_year(self._h, slot, jyear), "h9g_run_year")
+
+    def run_site(self, sub, daily, lai, raise_on_stop: bool = True) -> np.ndarray:
+        """LCLIM site path (HYBRID9.f90:339-480) over nday days, synchronous.
+
+        sub (nday*nisurf, 5, ncell): tak (degC), rh, Rnet, PAR, ppt (mm per
+        substep); daily (nday, 2, ncell): huss, ps; lai (nday, 3, ncell):
+        (LAI, a, b), NaN = unchanged.  Returns the daily diagnostics
+        (nday, 11, ncell), site.DIAG_FIELDS (NaN for masked/failed cells)."""
+        daily = np.ascontiguousarray(daily, dtype=np.float32)
+        nday = daily.shape[0]
+        sub = np.ascontiguousarray(sub, dtype=np.float32)
+        lai = np.ascontiguousarray(lai, dtype=np.float32)
+        if (sub.shape != (nday * self.nisurf, 5, self.ncell) or daily.shape != (nday, 2, self.ncell)
+                or lai.shape != (nday, 3, self.ncell)):
+            raise ValueError("run_site: shapes must be sub (nday*nisurf, 5, ncell), "
+                             "daily (nday, 2, ncell), lai (nday, 3, ncell)")
+        out = np.empty((nday, 11, self.ncell), dtype=np.float32)
+        rc = _check(self._lib.h9g_run_site(self._h, nday, _fp(sub), _fp(daily), _fp(lai), _fp(out)),
+                    "h9g_run_site")
+        if rc and raise_on_stop:
+            raise ReferenceStop(self.last_error())
+        self.site_rc = rc
+        return out
 
     def sync(self, raise_on_stop: bool = True) -> int:
         rc = _check(self._lib.h9g_sync(self._h), "h9g_sync")

@@ -271,6 +271,88 @@ h9g_solo_kernel(const KArgs a, const G g) {
   }
 }
 
+// LCLIM single-site kernel (HYBRID9.f90:339-480): one lane per site,
+// cell_site of h9g_pair.h.  Parameters and state as the year kernels.
+struct SiteArgs {
+  int ncell, nday, nisurf;
+  const float *__restrict__ par;
+  float *__restrict__ st;
+  const float *__restrict__ sub, *__restrict__ daily, *__restrict__ lai;
+  float *__restrict__ out;
+  int *__restrict__ err;
+  int *__restrict__ err_flag;
+};
+
+template <int L, class G>
+__global__ void __launch_bounds__(64) h9g_site_kernel(const SiteArgs a, const G g) {
+  typedef SoloStore<L> SS;
+  __shared__ uint64_t s_e2[32];
+  __shared__ double s_l2[32];
+  __shared__ float s_cell[SS::ROWS * 64];
+  __shared__ float s_zt[2 * (L + 2)];
+  if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
+  load_tabs(s_e2, s_l2);
+  const h9m::Tabs T = {s_e2, s_l2};
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.ncell) return;
+  const int n = a.ncell;
+  SS cs{(lds_float *)&s_cell[threadIdx.x], (const lds_float *)s_zt};
+  St<L> s;
+#pragma unroll
+  for (int p = 0; p < 4; p++)
+#pragma unroll
+    for (int i = 1; i <= L; i++) cs.set_lay(p, i, a.par[(size_t)(p * L + i - 1) * n + c]);
+  cs.set_sc(PS_FMAX, a.par[(size_t)(4 * L) * n + c]);
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    s.h2o[i] = a.st[(size_t)(0 * L + i - 1) * n + c];
+    s.smp[i] = a.st[(size_t)(2 * L + i - 1) * n + c];
+    cs.set_lay(PF_ROOTR, i, a.st[(size_t)(3 * L + i - 1) * n + c]);
+  }
+  const float h2o_ma1 = a.st[(size_t)(1 * L) * n + c];
+  const size_t o8 = (size_t)(4 * L + 1) * n + c;
+  s.zwt = a.st[o8 + 0 * (size_t)n];
+  s.wa = a.st[o8 + 1 * (size_t)n];
+  s.LAI = a.st[o8 + 2 * (size_t)n];
+  s.LAI_litter = a.st[o8 + 3 * (size_t)n];
+  s.pm = a.st[o8 + 4 * (size_t)n];
+  s.pfm = a.st[o8 + 5 * (size_t)n];
+  s.plen = a.st[o8 + 6 * (size_t)n];
+  s.rdepth = a.st[o8 + 7 * (size_t)n];
+  float ts_sum = zero;
+#pragma unroll
+  for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.lay(PF_TS, i);
+  if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
+    for (int d = 0; d < a.nday; d++)
+      for (int r = 0; r < 11; r++) a.out[((size_t)d * 11 + r) * n + c] = __builtin_nanf("");
+    return;
+  }
+  cell_inv_pair<L, G>(g, cs);
+  int eday = 0, estep = 0;
+  float errval = 0.0f;
+  const int code = cell_site<L, G, SS>(g, cs, s, h2o_ma1, a.sub + c, a.daily + c, a.lai + c, a.out + c,
+                                       (size_t)n, a.nday, a.nisurf, eday, estep, errval, T);
+  const size_t ow = (size_t)(4 * L + 1) * n + c;
+#pragma unroll
+  for (int i = 1; i <= L; i++) {
+    a.st[(size_t)(0 * L + i - 1) * n + c] = s.h2o[i];
+    a.st[(size_t)(2 * L + i - 1) * n + c] = s.smp[i];
+  }
+  a.st[ow + 0 * (size_t)n] = s.zwt;
+  a.st[ow + 1 * (size_t)n] = s.wa;
+  a.st[ow + 2 * (size_t)n] = s.LAI;
+  a.st[ow + 3 * (size_t)n] = s.LAI_litter;
+  if (code) {
+    a.err[0 * (size_t)n + c] = code;
+    a.err[1 * (size_t)n + c] = eday;
+    a.err[2 * (size_t)n + c] = estep;
+    a.err[3 * (size_t)n + c] = __builtin_bit_cast(int, errval);
+    atomicOr(a.err_flag, 1);
+    for (int d = eday; d < a.nday; d++)
+      for (int r = 0; r < 11; r++) a.out[((size_t)d * 11 + r) * n + c] = __builtin_nanf("");
+  }
+}
+
 template <int L, class G>
 __global__ void __launch_bounds__(H9G_BLOCK) h9g_init_kernel(int ncell, const float *__restrict__ par,
                                                              float *__restrict__ st, const G g) {
@@ -943,6 +1025,49 @@ int h9g_sync(h9g_ctx *ctx) {
     }
   }
   return ctx->last_err.code;
+}
+
+int h9g_run_site(h9g_ctx *ctx, int nday, const float *sub, const float *daily, const float *lai, float *diag) {
+  if (!ctx || nday <= 0 || !sub || !daily || !lai || !diag) return H9G_EINVAL;
+  if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  const size_t n = ctx->n, ns = (size_t)ctx->cfg.nisurf;
+  const size_t nsub = (size_t)nday * ns * 5 * n, nd = (size_t)nday * 2 * n, nl = (size_t)nday * 3 * n;
+  const size_t nout = (size_t)nday * 11 * n;
+  float *buf = nullptr;
+  HIPCHK(hipMalloc(&buf, sizeof(float) * (nsub + nd + nl + nout)));
+  SiteArgs a;
+  a.ncell = (int)n;
+  a.nday = nday;
+  a.nisurf = ctx->cfg.nisurf;
+  a.par = ctx->d_par;
+  a.st = ctx->d_st;
+  a.sub = buf;
+  a.daily = buf + nsub;
+  a.lai = buf + nsub + nd;
+  a.out = buf + nsub + nd + nl;
+  a.err = ctx->d_err;
+  a.err_flag = ctx->d_errflag;
+  int rc = 0;
+  hipError_t e = hipMemcpy(buf, sub, sizeof(float) * nsub, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(buf + nsub, daily, sizeof(float) * nd, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(buf + nsub + nd, lai, sizeof(float) * nl, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    H9G_DISPATCH(ctx, h9g_site_kernel, (unsigned)((n + 63) / 64), 64, ctx->sc, a);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->sc);
+  if (e == hipSuccess) e = hipMemcpy(diag, a.out, sizeof(float) * nout, hipMemcpyDeviceToHost);
+  (void)hipFree(buf);
+  if (e != hipSuccess) {
+    fprintf(stderr, "h9g: h9g_run_site failed: %s\n", hipGetErrorString(e));
+    return H9G_EHIP;
+  }
+  ctx->last_year = 0;      // error records of a site run: day counts from the start of the run
+  ctx->ran = 1;
+  rc = h9g_sync(ctx);
+  return rc;
 }
 
 int h9g_last_error(h9g_ctx *ctx, h9g_error *err) {

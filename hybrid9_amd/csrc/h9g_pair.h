@@ -160,8 +160,16 @@ struct SoloStore {
 };
 
 // Phase profiler (tools: H9G_STAMPS build only).  NoProf compiles away.
+// flux(evg, tran) receives the substep's qflx_evap_grnd and
+// qflx_tran_veg_col (HYDROLOGY.f90:388-400); only the site path keeps them.
 struct NoProf {
   H9K_HD void mark(int) {}
+  H9K_HD void flux(float, float) {}
+};
+struct FluxProf {
+  float evg, tran;
+  H9K_HD void mark(int) {}
+  H9K_HD void flux(float e, float t) { evg = e; tran = t; }
 };
 #if defined(H9G_STAMPS)
 H9K_HD uint64_t stamp_clock() {
@@ -179,6 +187,7 @@ struct StampProf {                     // wave-uniform shader-clock deltas per p
     acc[k] += (uint32_t)(t - last);
     last = t;
   }
+  H9K_HD void flux(float, float) {}
 };
 #endif
 
@@ -391,6 +400,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   float em1 = m.div(g.dz(1) * (theta[1] - watmin), dt, g.rdt()) - tran * ROOT(1);
   em1 = MAXF(zero, em1);
   evg = MINF(em1, evg);
+  pr.flux(evg, tran);
   // :426-478
   const float qflx_evap = evg;
   float qflx_in_soil = (one - frac_h2osfc) * (qflx_top_soil - qflx_surf);
@@ -924,6 +934,65 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float
   A[A_EVAP * as] = zero / (float)(nt * nisurf);
 #pragma unroll
   for (int k = A_TAS; k <= A_H2O; k++) A[k * as] = A[k * as] / (float)nt;
+  return 0;
+}
+
+// LCLIM single-site days for one cell (HYBRID9.f90:353-478): per-substep
+// forcing, the day-of-year LAI schedule, no GROW.  Every substep runs the
+// exact path (MathExact, one lane for all layers): this is the one-site
+// evaluation tool, not the grid path.  Layouts (n = cells, [row][cell]):
+//   sub   (nday*nisurf, 5, n): tak (degC), rh, Rnet, PAR, ppt (mm per substep)  :428-439
+//   daily (nday, 2, n): huss, ps                                                 :377-378
+//   lai   (nday, 3, n): LAI, a, b -- LAI = LAI, LAI_litter = LAI_litter + a - b,
+//         NaN = no change (the schedule of :380-417)
+//   out   (nday, 11, n): evap_day, evap_grnd_day, theta(1:4), theta_ma(1), LAI,
+//         LAI_litter, w_i, fT                                                    :464-469
+// w_i and fT are GROW's and GROW never runs here: they are 0.
+template <int L, class G, class CS>
+H9K_HD int cell_site(const G &g, CS cs, St<L> &s, float h2o_ma1, const float *sub, const float *daily,
+                     const float *lai, float *out, size_t n, int nday, int nisurf, int &eday, int &estep,
+                     float &errval, const h9m::Tabs &T) {
+  MathExact me{T};
+  const SplitAll sp;
+  FluxProf fx{zero, zero};
+  float rnf_sum = zero;
+  const float dt = g.dt();
+  const float theta_ma1 = h2o_ma1 / g.thk(1);                         // HYDROLOGY.f90:149
+  for (int day = 0; day < nday; day++) {
+    const float *l = lai + (size_t)day * 3 * n;
+    if (l[0] == l[0]) s.LAI = l[0];
+    if (l[n] == l[n]) s.LAI_litter = s.LAI_litter + l[n] - l[2 * n];
+    const float *dd = daily + (size_t)day * 2 * n;
+    float evap_day = zero, evap_grnd_day = zero;
+    for (int ns = 0; ns < nisurf; ns++) {
+      const float *v = sub + ((size_t)day * nisurf + ns) * 5 * n;
+      Day d;
+      d.tak = v[0] + tf;
+      d.rh = v[n];
+      d.Rnet = v[2 * n];
+      d.PAR = v[3 * n];
+      d.forc_rain = v[4 * n] / dt;
+      d.lamb = ((2503.0f - 2.386f * (d.tak - tf))) * 1.0E3f;        // :445
+      d.huss = dd[0];
+      d.ps = dd[n];
+      day_consts(d, s.LAI, s.LAI_litter, cs, me);
+      const int code = hydrology_pair<L, G, MathExact, SplitAll, CS, FluxProf>(g, cs, sp, s, rnf_sum, errval,
+                                                                            me, fx);
+      if (code) { eday = day; estep = ns; return code; }
+      evap_day = evap_day + (fx.evg + fx.tran) * dt;                  // :457-458
+      evap_grnd_day = evap_grnd_day + fx.evg * dt;
+    }
+    float *o = out + (size_t)day * 11 * n;
+    o[0] = evap_day;
+    o[n] = evap_grnd_day;
+#pragma unroll
+    for (int i = 1; i <= 4; i++) o[(1 + i) * n] = MAXF(s.h2o[i], 1.0E-6f) / g.thk(i);   // :1233
+    o[6 * n] = theta_ma1;
+    o[7 * n] = s.LAI;
+    o[8 * n] = s.LAI_litter;
+    o[9 * n] = zero;
+    o[10 * n] = zero;
+  }
   return 0;
 }
 

@@ -229,6 +229,15 @@ INTERFACE
     REAL(C_FLOAT) :: theta_s (*), hksat (*), bsw (*), psi_s (*), fmax (*)
     INTEGER(C_INT) :: h9g_get_params
   END FUNCTION
+  ! LCLIM single-site path (HYBRID9.f90:339-480): sub (cells, 5, nday*NISURF),
+  ! daily (cells, 2, nday), lai (cells, 3, nday), diag (cells, 11, nday)
+  FUNCTION h9g_run_site (ctx, nday, sub, daily, lai, diag) BIND(C, NAME='h9g_run_site')
+    IMPORT :: C_INT, C_PTR, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT), VALUE :: nday
+    REAL(C_FLOAT) :: sub (*), daily (*), lai (*), diag (*)
+    INTEGER(C_INT) :: h9g_run_site
+  END FUNCTION
   FUNCTION h9g_last_kernel_ms (ctx) BIND(C, NAME='h9g_last_kernel_ms')
     IMPORT :: C_PTR, C_FLOAT
     TYPE(C_PTR), VALUE :: ctx

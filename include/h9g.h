@@ -120,6 +120,26 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear);
 int h9g_sync(h9g_ctx *ctx);
 int h9g_last_error(h9g_ctx *ctx, h9g_error *err);
 
+/* --- LCLIM single-site path (HYBRID9.f90:339-480) ---------------------- */
+/* Runs nday days of the site path for every cell of the context: per
+ * substep forcing, a day-of-year LAI schedule, HYDROLOGY only (no GROW).
+ * Replaces the LCLIM branch :339-480 (its CSV reads :353-439 are done by
+ * the caller, e.g. hybrid9_amd.site.read_lclim).  Host arrays, [row][cell]:
+ *   sub   (nday*nisurf, 5, ncell): tak (degC), rh (%), Rnet (W m-2),
+ *         PAR, ppt (mm per substep)        -- LCLIM_array2 (22,25,14,16,35)
+ *   daily (nday, 2, ncell): huss (kg/kg), ps (Pa)   -- LCLIM_array (5,6)
+ *   lai   (nday, 3, ncell): (LAI, a, b): LAI = LAI, then
+ *         LAI_litter = LAI_litter + a - b; NaN leaves a value unchanged
+ *         (encodes the schedule of :380-417)
+ *   diag  (nday, 11, ncell) out: evap_day, evap_grnd_day, theta(1:4),
+ *         theta_ma(1), LAI, LAI_litter, w_i, fT (the daily line :464-469;
+ *         w_i = fT = 0 as GROW does not run; NaN for masked/failed cells)
+ * Synchronous.  Updates the state (h2osoi_liq, smp, zwt, wa, LAI,
+ * LAI_litter).  Returns 0 or a STOP code (h9g_last_error: day counts
+ * from the start of the run, year = 0). */
+int h9g_run_site(h9g_ctx *ctx, int nday, const float *sub, const float *daily,
+                 const float *lai, float *diag);
+
 /* --- outputs (HYBRID9.f90:263-290) ------------------------------------ */
 /* Annual means of the last year run, (12+L) rows of (ncell):
  * npp plant_mass rnf evap tas rlds rsds huss ps pr rhs theta(1..L)

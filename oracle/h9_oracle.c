@@ -778,6 +778,93 @@ int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
 }
 
 /* ----------------------------------------------------------------------
+ * LCLIM single-site path, HYBRID9.f90:353-478: per-substep forcing
+ * (:428-445), the day-of-year LAI schedule (:380-417) as (LAI, a, b) rows
+ * (NaN = no change; LAI_litter = LAI_litter + a - b), no GROW, and the
+ * daily diagnostics of :464-469.  Layouts as h9g_run_site (include/h9g.h):
+ * sub (nday*nisurf, 5, ncell), daily (nday, 2, ncell), lai (nday, 3, ncell),
+ * diag out (nday, 11, ncell).  Pinned against oracle/_ref/h9ref's
+ * lclim_mode through tests/golden/lclim_*.npz.
+ * -------------------------------------------------------------------- */
+int h9o_site(int ncell, int L, int nisurf, int nday, const float *zi, const float *params,
+             const float *sub, const float *daily, const float *lai, float *state, float *diag,
+             int nthreads, h9o_error *err) {
+  if (ncell < 0 || L < 4 || L > LM || nisurf < 1 || nday < 1) return H9O_ERR_ARGS;
+  const size_t n = (size_t)ncell;
+  int first_code = 0, first_cell = ncell;
+  h9o_error first = {0, -1, -1, -1, 0.0f};
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1) if (nthreads != 1)
+  for (int c = 0; c < ncell; c++) {
+    geom_t g;
+    geom_init(&g, L, nisurf, zi);
+    par_t p;
+    st_t s;
+    load_par(&p, params, ncell, L, c);
+    load_st(&s, state, ncell, L, c);
+    float ts_sum = zero;
+    for (int i = 1; i <= L; i++) ts_sum = ts_sum + p.theta_s[i];
+    if (!(ts_sum > trunc_)) continue;
+    float theta[LM + 2] = {0};
+    float rnf_sum = zero, errval = 0.0f;
+    int code = 0, eday = -1, estep = -1;
+    for (int day = 0; day < nday && !code; day++) {
+      const float *l = lai + (size_t)day * 3 * n + c;
+      if (l[0] == l[0]) s.LAI = l[0];                                   /* :380-417 */
+      if (l[n] == l[n]) s.LAI_litter = s.LAI_litter + l[n] - l[2 * n];
+      float evap_day = zero, evap_grnd_day = zero;                      /* :421-422 */
+      for (int ns = 0; ns < nisurf; ns++) {
+        const float *v = sub + ((size_t)day * nisurf + ns) * 5 * n + c;
+        day_t d;
+        d.tak = v[0] + tf;                                              /* :430-439 */
+        d.tas = d.tak;
+        d.rh = v[n];
+        d.Rnet = v[2 * n];
+        d.PAR = v[3 * n];
+        d.forc_rain = v[4 * n] / g.dt;
+        d.lamb = ((2503.0f - 2.386f * (d.tak - tf))) * 1.0E3f;         /* :445 */
+        d.huss = daily[(size_t)day * 2 * n + c];                        /* :377-378 */
+        d.ps = daily[(size_t)day * 2 * n + n + c];
+        float tran, evg;
+        code = hydrology(&g, &p, &d, &s, &rnf_sum, theta, &tran, &evg, &errval);   /* :453 */
+        if (code) { eday = day; estep = ns; break; }
+        evap_day = evap_day + (evg + tran) * g.dt;                      /* :457-458 */
+        evap_grnd_day = evap_grnd_day + evg * g.dt;
+      }
+      float *o = diag + (size_t)day * 11 * n + c;                       /* :464-469 */
+      if (code) {
+        for (int k = 0; k < 11; k++) o[k * n] = NAN;
+        break;
+      }
+      o[0] = evap_day;
+      o[n] = evap_grnd_day;
+      for (int i = 1; i <= 4; i++) o[(1 + i) * n] = theta[i];
+      o[6 * n] = s.h2o_ma[1] / (g.dz[1] * rhow / 1.0E3f);             /* HYDROLOGY.f90:149 */
+      o[7 * n] = s.LAI;
+      o[8 * n] = s.LAI_litter;
+      o[9 * n] = zero;                                                  /* w_i, fT: no GROW */
+      o[10 * n] = zero;
+    }
+    store_st(&s, state, ncell, L, c);
+    if (code) {
+#pragma omp critical(h9o_err)
+      {
+        if (c < first_cell) {
+          first_cell = c;
+          first_code = code;
+          first.code = code;
+          first.cell = c;
+          first.day = eday;
+          first.substep = estep;
+          first.value = errval;
+        }
+      }
+    }
+  }
+  if (err) *err = first;
+  return first_code;
+}
+
+/* ----------------------------------------------------------------------
  * Soil parameter build, INIT.f90:575-631 (one soil layer) and :661-680
  * (Fmax), for the 0.5-degree cells gid (iy*nx+ix, row iy from the north).
  * Input fields are the 30" layers as read at INIT.f90:540-569: ny*60 rows

@@ -63,6 +63,13 @@ int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
             float *state, float *annual, int ntrace, const int *trace_cells,
             float *trace, int nthreads, h9o_error *err);
 
+/* LCLIM single-site path (HYBRID9.f90:339-480), layouts of h9g_run_site:
+ * sub (nday*nisurf, 5, ncell), daily (nday, 2, ncell), lai (nday, 3, ncell),
+ * diag out (nday, 11, ncell); state in/out.  Returns 0 or the first STOP. */
+int h9o_site(int ncell, int L, int nisurf, int nday, const float *zi, const float *params,
+             const float *sub, const float *daily, const float *lai, float *state, float *diag,
+             int nthreads, h9o_error *err);
+
 /* Soil parameter build (INIT.f90:575-631 one layer, :661-680 Fmax). */
 void h9o_soil_layer(int nx, int ny, int ncell, const int64_t *gid, const float *ts_in,
                     const float *ks_in, const float *lm_in, const float *ps_in, float *theta_s,

@@ -40,6 +40,7 @@ def lib():
         _lib.h9o_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  f, f, f, f, f, C.c_int, C.POINTER(C.c_int), f,
                                  C.c_int, C.POINTER(H9OError)]
+        _lib.h9o_site.argtypes = [C.c_int] * 4 + [f] * 7 + [C.c_int, C.POINTER(H9OError)]
         i64 = C.POINTER(C.c_int64)
         _lib.h9o_soil_layer.argtypes = [C.c_int, C.c_int, C.c_int, i64, f, f, f, f, f, f, f, f]
         _lib.h9o_soil_fmax.argtypes = [C.c_int, C.c_int, i64, C.POINTER(C.c_int32),
@@ -93,6 +94,28 @@ def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=1,
     if len(tc):
         out["trace"] = tr
     return out
+
+
+def site(*, zi, params, sub, daily, lai, nisurf=48, state0=None, nthreads=1):
+    """LCLIM site path restated (h9o_site); same contract as
+    refcase.run_site_case; returns dict(daily, state, rc, err).  Masked and
+    failed cells: NaN rows."""
+    L = params["theta_s"].shape[1]
+    n = params["fmax"].size
+    zi = np.ascontiguousarray(zi, dtype=np.float32)
+    pp = pack_params(params)
+    st = init_state(params, zi) if state0 is None else refcase.pack_state(state0, L)
+    sub = np.ascontiguousarray(sub, dtype=np.float32)
+    daily = np.ascontiguousarray(daily, dtype=np.float32)
+    lai = np.ascontiguousarray(lai, dtype=np.float32)
+    nday = daily.shape[0]
+    out = np.full((nday, 11, n), np.nan, dtype=np.float32)
+    err = H9OError()
+    rc = lib().h9o_site(n, L, nisurf, nday, _fp(zi), _fp(pp), _fp(sub), _fp(daily), _fp(lai),
+                        _fp(st), _fp(out), nthreads, C.byref(err))
+    return dict(daily=out, state=refcase.unpack_state(st, n, L), rc=rc,
+                err=dict(code=err.code, cell=err.cell, day=err.day, substep=err.substep,
+                         value=err.value))
 
 
 def soil_layer(nx, ny, gid, ts, ks, lm, ps):

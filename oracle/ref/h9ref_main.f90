@@ -22,6 +22,14 @@ PROGRAM H9REF
 !   * grow_on=0 skips CALL GROW (hydrology-only configs, as the LCLIM
 !     path does at HYBRID9.f90:475).
 !
+! lclim_mode /= 0 restates instead the LCLIM single-site path of
+! HYBRID9.f90:339-480: sub-daily forcing (tak, rh, Rnet, PAR, ppt per
+! substep, :428-439), daily huss and ps (:377-378), the day-of-year LAI
+! schedule (:380-417, given as (LAI, a, b): LAI = LAI; LAI_litter =
+! LAI_litter + a - b), no GROW (:475), and the daily diagnostics of
+! :464-469 (evap_day, evap_grnd_day, theta(1:4), theta_ma(1), LAI,
+! LAI_litter, w_i, fT) instead of annual means.
+!
 ! Files in <dir> (see oracle/README.md for the byte layout):
 !   case.nml  namelist /h9case/
 !   zi.f32    zi(0:Nlevgrnd)                       (Nlevgrnd+1 floats)
@@ -34,7 +42,8 @@ USE CONTROL
 USE SHARED
 IMPLICIT NONE
 
-INTEGER :: ncell, year0, nyears, grow_on, state_override, ntrace
+INTEGER :: ncell, year0, nyears, grow_on, state_override, ntrace, lclim_mode
+REAL, ALLOCATABLE :: lsub (:,:,:), lday (:,:,:), llai (:,:,:), out_day (:,:,:)
 INTEGER :: trace_cells (64)
 INTEGER :: ndays, iyr, itr, L, u, ios
 LOGICAL :: do_trace
@@ -49,13 +58,13 @@ REAL :: ps_sum, pr_sum, rhs_sum, h2osoi_sum_total
 INTEGER :: nfield
 
 NAMELIST /h9case/ ncell, NISURF, year0, nyears, grow_on, &
-                  state_override, ntrace, trace_cells
+                  state_override, ntrace, trace_cells, lclim_mode
 
 CALL GET_COMMAND_ARGUMENT (1, dir)
 IF (LEN_TRIM (dir) == 0) STOP 'usage: h9ref <casedir>'
 
 ncell = 0; NISURF = 48; year0 = 1901; nyears = 1; grow_on = 1
-state_override = 0; ntrace = 0; trace_cells = 0
+state_override = 0; ntrace = 0; trace_cells = 0; lclim_mode = 0
 OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/case.nml', STATUS='OLD')
 READ (u, NML=h9case)
 CLOSE (u)
@@ -158,10 +167,35 @@ OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/params.f32', ACCESS='STREAM', &
       FORM='UNFORMATTED', STATUS='OLD')
 READ (u) theta_s, hksat, bsw, psi_s, Fmax
 CLOSE (u)
-OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/forcing.f32', ACCESS='STREAM', &
-      FORM='UNFORMATTED', STATUS='OLD')
-READ (u) tas, rlds, rsds, huss, ps, pr, rhs
-CLOSE (u)
+IF (lclim_mode == 0) THEN
+  OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/forcing.f32', ACCESS='STREAM', &
+        FORM='UNFORMATTED', STATUS='OLD')
+  READ (u) tas, rlds, rsds, huss, ps, pr, rhs
+  CLOSE (u)
+ELSE
+  ! lclim_sub.f32: (ncell, 5, NISURF*ndays): tak(degC) rh Rnet PAR ppt(mm/step)
+  ! lclim_day.f32: (ncell, 2, ndays): huss ps;  lclim_lai.f32: (ncell, 3, ndays)
+  ALLOCATE (lsub (lon_c, 5, NISURF*NTIMES), lday (lon_c, 2, NTIMES))
+  ALLOCATE (llai (lon_c, 3, NTIMES), out_day (lon_c, 11, NTIMES))
+  OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/lclim_sub.f32', ACCESS='STREAM', &
+        FORM='UNFORMATTED', STATUS='OLD')
+  READ (u) lsub
+  CLOSE (u)
+  OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/lclim_day.f32', ACCESS='STREAM', &
+        FORM='UNFORMATTED', STATUS='OLD')
+  READ (u) lday
+  CLOSE (u)
+  OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/lclim_lai.f32', ACCESS='STREAM', &
+        FORM='UNFORMATTED', STATUS='OLD')
+  READ (u) llai
+  CLOSE (u)
+  DO I = 1, NTIMES
+    huss (:,1,I) = lday (:,1,I)
+    ps (:,1,I) = lday (:,2,I)
+  END DO
+  tas = zero; rlds = zero; rsds = zero; pr = zero; rhs = zero
+  out_day = zero
+END IF
 
 !----------------------------------------------------------------------!
 ! Initial state (INIT.f90:707-811), macroporosity 0.1 (INIT.f90:620).
@@ -230,6 +264,55 @@ IF (ntrace > 0) THEN
         FORM='UNFORMATTED', STATUS='REPLACE')
 END IF
 npp = zero
+
+!----------------------------------------------------------------------!
+! LCLIM single-site path, restating HYBRID9.f90:353-478 for every cell.
+!----------------------------------------------------------------------!
+IF (lclim_mode /= 0) THEN
+DO y = 1, lat_c
+  DO x = 1, lon_c
+    IF (SUM (theta_s (:,x,y)) > trunc) THEN
+      smp (:) = fz ((x-1)*L+1 : x*L)          ! isolated-cell semantics
+      nlayers = nsoil_layers_max
+      DO jyear = syr, eyr
+        DO iTIME = time_BOY (jyear-1859), time_BOY (jyear+1-1859) - 1
+          iT = iTIME-time_BOY(syr-1859) + 1
+          IF (llai (x,1,iT) == llai (x,1,iT)) LAI (x,y) = llai (x,1,iT)          ! :380-417
+          IF (llai (x,2,iT) == llai (x,2,iT)) &
+            LAI_litter (x,y) = LAI_litter (x,y) + llai (x,2,iT) - llai (x,3,iT)
+          evap_day = zero
+          evap_grnd_day = zero
+          DO NS = 1, NISURF
+            tak  = lsub (x,1,(iT-1)*NISURF+NS) + tf                               ! :430-439
+            rh   = lsub (x,2,(iT-1)*NISURF+NS)
+            Rnet = lsub (x,3,(iT-1)*NISURF+NS)
+            PAR  = lsub (x,4,(iT-1)*NISURF+NS)
+            ppt  = lsub (x,5,(iT-1)*NISURF+NS) / dt
+            forc_rain = ppt
+            lamb = ((2503.0 - 2.386 * (tak - tf))) * 1.0E3                        ! :445
+            CALL HYDROLOGY                                                         ! :453
+            evap_day = evap_day + (qflx_evap_grnd + qflx_tran_veg_col) * dt        ! :457
+            evap_grnd_day = evap_grnd_day + qflx_evap_grnd * dt                    ! :458
+          END DO
+          out_day (x, 1, iT) = evap_day                                           ! :464-469
+          out_day (x, 2, iT) = evap_grnd_day
+          out_day (x, 3:6, iT) = theta (1:4)
+          out_day (x, 7, iT) = theta_ma (1)
+          out_day (x, 8, iT) = LAI (x,y)
+          out_day (x, 9, iT) = LAI_litter (x,y)
+          out_day (x, 10, iT) = w_i
+          out_day (x, 11, iT) = fT
+        END DO
+      END DO
+      fz ((x-1)*L+1 : x*L) = smp (:)
+    END IF
+  END DO
+END DO
+OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/daily.f32', ACCESS='STREAM', &
+      FORM='UNFORMATTED', STATUS='REPLACE')
+WRITE (u) out_day
+CLOSE (u)
+ELSE
 
 !----------------------------------------------------------------------!
 ! Hot loops, restating HYBRID9.f90:120-290 (PGF path).
@@ -333,6 +416,7 @@ OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/annual.f32', ACCESS='STREAM', &
       FORM='UNFORMATTED', STATUS='REPLACE')
 WRITE (u) out_ann
 CLOSE (u)
+END IF   ! lclim
 OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/state_end.f32', ACCESS='STREAM', &
       FORM='UNFORMATTED', STATUS='REPLACE', IOSTAT=ios)
 WRITE (u) h2osoi_liq, h2osoi_liq_ma, fz, rootr_col, zwt, wa, LAI, &

@@ -64,8 +64,8 @@ def unpack_state(buf: np.ndarray, ncell: int, L: int) -> dict:
     return out
 
 
-def write_case(d, *, zi, params, forcing, nisurf=48, year0=1901, nyears=1,
-               grow_on=1, state0=None, trace_cells=()):
+def write_case(d, *, zi, params, forcing=None, nisurf=48, year0=1901, nyears=1,
+               grow_on=1, state0=None, trace_cells=(), site=None):
     d = Path(d)
     d.mkdir(parents=True, exist_ok=True)
     ncell = params["fmax"].size
@@ -74,12 +74,17 @@ def write_case(d, *, zi, params, forcing, nisurf=48, year0=1901, nyears=1,
     nml = ("&h9case\n"
            f" ncell={ncell}, NISURF={nisurf}, year0={year0}, nyears={nyears},\n"
            f" grow_on={int(grow_on)}, state_override={int(state0 is not None)},\n"
-           f" ntrace={len(trace_cells)}, trace_cells={','.join(str(c + 1) for c in tc)}\n/\n")
+           f" ntrace={len(trace_cells)}, trace_cells={','.join(str(c + 1) for c in tc)},\n"
+           f" lclim_mode={int(site is not None)}\n/\n")
     (d / "case.nml").write_text(nml)
     np.asarray(zi, dtype=np.float32).tofile(d / "zi.f32")
     np.concatenate([params[k].ravel() for k in ("theta_s", "hksat", "bsw", "psi_s")]
                    + [params["fmax"].ravel()]).astype(np.float32).tofile(d / "params.f32")
-    np.ascontiguousarray(forcing, dtype=np.float32).tofile(d / "forcing.f32")
+    if site is None:
+        np.ascontiguousarray(forcing, dtype=np.float32).tofile(d / "forcing.f32")
+    else:   # LCLIM mode (h9ref_main.f90): sub (T, 5, n), daily (nday, 2, n), lai (nday, 3, n)
+        for k in ("sub", "daily", "lai"):
+            np.ascontiguousarray(site[k], dtype=np.float32).tofile(d / f"lclim_{'day' if k == 'daily' else k}.f32")
     if state0 is not None:
         pack_state(state0, L).tofile(d / "state0.f32")
 
@@ -122,7 +127,7 @@ def run_ref(d, timeout=3600):
                        timeout=timeout)
     if "Fortran STOP" in (r.stdout + r.stderr) or "Problem" in r.stdout:
         raise RefStop(r.stdout)
-    if r.returncode != 0 or not (Path(d) / "annual.f32").exists():
+    if r.returncode != 0 or not ((Path(d) / "annual.f32").exists() or (Path(d) / "daily.f32").exists()):
         raise RuntimeError(f"h9ref failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
     return r
 
@@ -136,6 +141,21 @@ def read_outputs(d, ncell, L, nyears, ntrace=0):
         tr = np.fromfile(d / "trace.f32", dtype=np.float32)
         out["trace"] = tr.reshape(ntrace, -1, trace_width(L))
     return out
+
+
+def run_site_case(*, zi, params, sub, daily, lai, nisurf=48, year0=2002, nyears=2, state0=None):
+    """LCLIM single-site path of the reference (HYBRID9.f90:339-480) through
+    the harness: returns dict(daily (nday, 11, ncell), state)."""
+    ncell = params["fmax"].size
+    L = params["theta_s"].shape[1]
+    with tempfile.TemporaryDirectory(prefix="h9ref_") as td:
+        write_case(td, zi=zi, params=params, nisurf=nisurf, year0=year0, nyears=nyears,
+                   grow_on=0, state0=state0, site=dict(sub=sub, daily=daily, lai=lai))
+        run_ref(td)
+        nday = np.asarray(daily).shape[0]
+        out = np.fromfile(Path(td) / "daily.f32", dtype=np.float32).reshape(nday, 11, ncell)
+        st = unpack_state(np.fromfile(Path(td) / "state_end.f32", dtype=np.float32), ncell, L)
+        return dict(daily=out, state=st)
 
 
 def run_case(**kw):

@@ -57,6 +57,24 @@ def load_golden(name):
     return meta, inputs, expected
 
 
+def load_site_golden(name):
+    """(meta, inputs, expected) of an LCLIM golden (tests/golden/make_golden.py
+    lclim_case); inputs regenerated and checked against the stored sha256."""
+    from tests.golden.make_golden import digest, packed_params, site_inputs
+
+    z = np.load(GOLDEN / f"{name}.npz")
+    meta = json.loads(str(z["meta"]))
+    gid = np.asarray(meta["gid"], dtype=np.int64)
+    years = tuple(range(meta["year0"], meta["year0"] + meta["nyears"]))
+    ev = None if meta["events"] is None else {int(k): v for k, v in meta["events"].items()}
+    p, sub, daily, lai = site_inputs(gid, meta["L"], meta["nisurf"], years, ev, meta["seed"],
+                                     meta["soils"], meta["ppt_scale"])
+    assert digest(packed_params(p), sub, daily, lai) == meta["input_sha256"], "site inputs drifted"
+    inputs = dict(zi=np.asarray(meta["zi"], np.float32), params=p, sub=sub, daily=daily, lai=lai,
+                  nisurf=meta["nisurf"])
+    return meta, inputs, dict(daily=z["daily"], state=z["state"])
+
+
 def same_bits(a, b):
     """Bitwise equality with NaN == NaN (any payload) and +0 == -0."""
     a = np.asarray(a)

@@ -92,3 +92,62 @@ extern "C" int h9k_host_run(int n, int L, int nisurf, int grow_on, int year0, in
   RP(10, make_geo_r<10>(zi, nisurf));
 #undef RP
 }
+
+// The LCLIM site path (cell_site of h9g_pair.h) on the host, same layouts as
+// h9g_run_site; state in the oracle's packed layout (as h9k_host_run).
+template <int L, class G>
+static int run_site_cells(const G &g, int n, int nday, int nisurf, const float *par, const float *sub,
+                          const float *daily, const float *lai, float *st, float *out, int *err) {
+  const h9m::Tabs T = {E2, L2};
+  int first = 0;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int c = 0; c < n; c++) {
+    float store[FlatStore<L>::N], zt[2 * (L + 2)];
+    fill_zt<L>(g, zt);
+    FlatStore<L> cs{store, zt};
+    St<L> s;
+    for (int i = 1; i <= L; i++) {
+      cs.set_lay(PF_TS, i, par[0 * n * L + c * L + i - 1]);
+      cs.set_lay(PF_HKS, i, par[1 * n * L + c * L + i - 1]);
+      cs.set_lay(PF_BSW, i, par[2 * n * L + c * L + i - 1]);
+      cs.set_lay(PF_PSI, i, par[3 * n * L + c * L + i - 1]);
+      s.h2o[i] = st[0 * n * L + c * L + i - 1];
+      s.smp[i] = st[2 * n * L + c * L + i - 1];
+      cs.set_lay(PF_ROOTR, i, st[3 * n * L + c * (L + 1) + i - 1]);
+    }
+    cs.set_sc(PS_FMAX, par[4 * n * L + c]);
+    cell_inv_pair<L, G>(g, cs);
+    float *q = st + (size_t)n * (4 * L + 1);
+    s.zwt = q[c]; s.wa = q[n + c]; s.LAI = q[2 * n + c]; s.LAI_litter = q[3 * n + c];
+    s.pm = q[4 * n + c]; s.pfm = q[5 * n + c]; s.plen = q[6 * n + c]; s.rdepth = q[7 * n + c];
+    int eday = 0, estep = 0;
+    float ev = 0;
+    const int code = cell_site<L, G>(g, cs, s, st[1 * n * L + c * L], sub + c, daily + c, lai + c, out + c,
+                                     (size_t)n, nday, nisurf, eday, estep, ev, T);
+    if (code) {
+      err[4 * c] = code; err[4 * c + 1] = 0; err[4 * c + 2] = eday; err[4 * c + 3] = estep;
+#pragma omp atomic write
+      first = code;
+    }
+    for (int i = 1; i <= L; i++) {
+      st[0 * n * L + c * L + i - 1] = s.h2o[i];
+      st[2 * n * L + c * L + i - 1] = s.smp[i];
+    }
+    q[c] = s.zwt; q[n + c] = s.wa; q[2 * n + c] = s.LAI; q[3 * n + c] = s.LAI_litter;
+  }
+  return first;
+}
+
+extern "C" int h9k_host_site(int n, int L, int nisurf, int nday, int use_const_geo, const float *zi,
+                             const float *par, const float *sub, const float *daily, const float *lai,
+                             float *st, float *out, int *err) {
+  const bool cg = use_const_geo != 0;
+#define RS(LL, G) return run_site_cells<LL>(G, n, nday, nisurf, par, sub, daily, lai, st, out, err)
+  if (L == 8) {
+    if (cg && nisurf == 48) RS(8, (GeoC<8, 48>()));
+    RS(8, make_geo_r<8>(zi, nisurf));
+  }
+  if (cg && nisurf == 48) RS(10, (GeoC<10, 48>()));
+  RS(10, make_geo_r<10>(zi, nisurf));
+#undef RS
+}

@@ -176,6 +176,70 @@ def edge_case():
     save("edge", meta, out, extra=dict(params=packed_params(p), forcing=f, state0=state0))
 
 
+def site_inputs(gid, L, nisurf, years, events, seed=synth.SEED, soils="synth", ppt_scale=1.0):
+    """Synthetic LCLIM site inputs (hybrid9_amd.site): soils of the land
+    cells gid (soils="independent": independent_layer_params), site forcing
+    (precipitation x ppt_scale), the day-of-year LAI schedule."""
+    from hybrid9_amd import site
+    p = synth.make_params(gid, L, seed) if soils == "synth" else independent_layer_params(gid, L, seed)
+    nd = sum(synth.days_in_year(y) for y in years)
+    sub, daily = site.synth_site(gid.size, nd, nisurf, seed, doy0=0)
+    sub[:, 4, :] *= np.float32(ppt_scale)
+    lai = site.broadcast(site.lai_schedule(years, events), gid.size)
+    return p, sub, daily, lai
+
+
+def lclim_case(name, gid, *, L=8, nisurf=48, years=(2002, 2003), events=None, stop=False,
+               soils="synth", ppt_scale=1.0):
+    """LCLIM single-site path (HYBRID9.f90:339-480) through the harness's
+    lclim_mode; events=None is the reference's Vaira LAI schedule.  stop:
+    the reference is expected to STOP; the fixture is what it prints."""
+    gid = np.asarray(gid, dtype=np.int64)
+    zi = synth.ZI_L8 if L == 8 else synth.ZI_L10
+    p, sub, daily, lai = site_inputs(gid, L, nisurf, years, events, soils=soils, ppt_scale=ppt_scale)
+    ev = None if events is None else {str(k): v for k, v in events.items()}
+    try:
+        out = refcase.run_site_case(zi=zi, params=p, sub=sub, daily=daily, lai=lai, nisurf=nisurf,
+                                    year0=years[0], nyears=len(years))
+        info = None
+    except refcase.RefStop as e:
+        if not stop:
+            raise
+        info = e.info
+    if stop:
+        if info is None:
+            raise SystemExit(f"{name}: expected a reference STOP")
+        out = dict(daily=np.zeros(0, np.float32), state=None)
+    meta = dict(name=name, kind="lclim_stop" if stop else "lclim", stop=info, seed=synth.SEED,
+                gid=gid.tolist(), L=L,
+                ncell=int(gid.size), year0=years[0], nyears=len(years), nisurf=nisurf, grow_on=0,
+                zi=zi.tolist(), events=ev, soils=soils, ppt_scale=ppt_scale, input_sha256=digest(packed_params(p), sub, daily, lai),
+                generator="oracle/_ref/h9ref lclim_mode (reference HYDROLOGY.f90, amdflang -O2)")
+    st = np.zeros(0, np.float32) if stop else refcase.pack_state(out["state"], L)
+    np.savez_compressed(OUT / f"{name}.npz", meta=np.array(json.dumps(meta)), daily=out["daily"],
+                        state=st)
+    print(f"{name}: {gid.size} sites x {len(years)} yr, {(OUT / f'{name}.npz').stat().st_size / 1e3:.0f} kB")
+
+
+# LAI schedule with litter moves on several days (lclim_ns24)
+LCLIM_EVENTS_2004 = {2004: [(10, 0.5, None), (60, 1.9, None), (100, 2.8, (0.2, 0.05)),
+                            (150, 1.1, (2.8, 1.1)), (200, 0.001, (1.1, 0.001)),
+                            (250, None, (0.0, 0.5)), (300, 0.4, None), (366, 0.7, (0.3, 0.3))]}
+
+
+def main_lclim():
+    land = synth.land_cells()
+    # the reference's Vaira configuration: 2002-2003, half-hourly, its LAI schedule
+    lclim_case("lclim_vaira", land[1000::9000][:6])
+    # NS=24, a leap year, another schedule (the reference's CONTROL.f90
+    # fixes nsoil_layers_max = 8: L=10 is checked against the C oracle)
+    g5 = land[4321::7000][:5]
+    lclim_case("lclim_ns24", g5, nisurf=24, years=(2004,), events=LCLIM_EVENTS_2004)
+    # a water-imbalance STOP (HYDROLOGY.f90:1244): hand-built soils, 10x rain
+    lclim_case("lclim_stop", land[263::527][90:98], nisurf=24, years=(2004,),
+               events=LCLIM_EVENTS_2004, stop=True, soils="independent", ppt_scale=10.0)
+
+
 def main():
     if not refcase.REF_BIN.exists():
         sys.exit("build the reference harness first: make -C oracle ref")
@@ -192,6 +256,7 @@ def main():
     # a reference STOP (water imbalance > 0.1 mm at NS=24) on hand-built soils
     stop_case("stop_ns24", land[263::527][90:98], nisurf=24)
     edge_case()
+    main_lclim()
 
 
 if __name__ == "__main__":
