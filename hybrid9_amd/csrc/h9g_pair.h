@@ -44,7 +44,8 @@ enum : int {
   PF_C3,                               // pte/(zi(I)-zi(I-1))
   PF_ROOTR,                            // rootr_col(1..L)
   PF_SVH2O, PF_SVSMP,                  // substep rollback
-  PF_N
+  PF_RPSI0, PF_RPSI1,                  // 1/(-psi) in double (recip64): low, high word
+  PF_N                                 //   (stores with kRecip only)
 };
 // per-cell fields
 enum : int {
@@ -78,6 +79,7 @@ H9K_HD float pair_swap(float v) {
 // ------------------------------------------------------------------ stores
 template <int L>
 struct FlatStore {                     // host: one flat array per cell
+  static constexpr bool kRecip = true;
   static constexpr int N = PF_N * L + PS_N;
   float *b;
   const float *zt;                     // zi(0..L+1), then zi(0..L+1)/1000
@@ -105,7 +107,11 @@ struct FlatStore {                     // host: one flat array per cell
 template <int L, int S>
 struct PairStore {
   static constexpr int NT = L / 2;
-  static constexpr int ROWS = PF_N * NT + (PS_N + 1) / 2;
+  // 3 workgroups per CU leave 76 rows per wave: the reciprocal rows fit at
+  // L = 8 (72 rows), not at L = 10 (75 rows without them)
+  static constexpr bool kRecip = L <= 8;
+  static constexpr int NPF = kRecip ? PF_N : PF_RPSI0;
+  static constexpr int ROWS = NPF * NT + (PS_N + 1) / 2;
   lds_float *self, *even;
   const lds_float *zt;                 // zi(0..L+1), then zi(0..L+1)/1000 (per block)
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
@@ -116,9 +122,9 @@ struct PairStore {
   __device__ __forceinline__ void set_lay(int p, int i, float v) const {
     even[(p * NT + ((i - 1) >> 1)) * S + ((i - 1) & 1)] = v;
   }
-  __device__ __forceinline__ float sc(int k) const { return even[(PF_N * NT + (k >> 1)) * S + (k & 1)]; }
+  __device__ __forceinline__ float sc(int k) const { return even[(NPF * NT + (k >> 1)) * S + (k & 1)]; }
   __device__ __forceinline__ void set_sc(int k, float v) const {
-    even[(PF_N * NT + (k >> 1)) * S + (k & 1)] = v;
+    even[(NPF * NT + (k >> 1)) * S + (k & 1)] = v;
   }
   __device__ __forceinline__ float slot(int p, int t) const { return self[(p * NT + t) * S]; }
   __device__ __forceinline__ void set_slot(int p, int t, float v) const { self[(p * NT + t) * S] = v; }
@@ -137,15 +143,17 @@ struct PairStore {
 // every field in the lane's own column.
 template <int L>
 struct SoloStore {
-  static constexpr int ROWS = PF_N * L + PS_N_NOPARK;   // 1054 waves = 5 blocks/CU: no plant parking
+  static constexpr bool kRecip = false;
+  static constexpr int NPF = PF_RPSI0;
+  static constexpr int ROWS = NPF * L + PS_N_NOPARK;   // 1054 waves = 5 blocks/CU: no plant parking
   lds_float *b;
   const lds_float *zt;
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
   __device__ __forceinline__ float lay(int p, int i) const { return b[(p * L + i - 1) * 64]; }
   __device__ __forceinline__ void set_lay(int p, int i, float v) const { b[(p * L + i - 1) * 64] = v; }
-  __device__ __forceinline__ float sc(int k) const { return b[(PF_N * L + k) * 64]; }
-  __device__ __forceinline__ void set_sc(int k, float v) const { b[(PF_N * L + k) * 64] = v; }
+  __device__ __forceinline__ float sc(int k) const { return b[(NPF * L + k) * 64]; }
+  __device__ __forceinline__ void set_sc(int k, float v) const { b[(NPF * L + k) * 64] = v; }
   __device__ __forceinline__ float slot(int p, int t) const { return b[(p * L + 2 * t) * 64]; }
   __device__ __forceinline__ void set_slot(int p, int t, float v) const { b[(p * L + 2 * t) * 64] = v; }
   __device__ __forceinline__ void launder() {
@@ -266,6 +274,30 @@ H9K_HD void save_layers(const Split2 &sp, const CS &cs, int p, const float *v) {
   for (int t = 0; t < L / 2; t++) cs.set_slot(p, t, sel(sp.h, v[2 * t + 1], v[2 * t + 2]));
 }
 
+// A double kept as two per-layer float fields (p: low word, p+1: high).
+H9K_HD double join_d(float lo, float hi) {
+  return __builtin_bit_cast(double, (uint64_t)__builtin_bit_cast(uint32_t, hi) << 32 |
+                                        __builtin_bit_cast(uint32_t, lo));
+}
+template <class CS>
+H9K_HD void set_lay_d(const CS &cs, int p, int i, double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  cs.set_lay(p, i, __builtin_bit_cast(float, (uint32_t)u));
+  cs.set_lay(p + 1, i, __builtin_bit_cast(float, (uint32_t)(u >> 32)));
+}
+template <class CS>
+H9K_HD double lay_d(const CS &cs, int p, int i) { return join_d(cs.lay(p, i), cs.lay(p + 1, i)); }
+
+// x / (-psi(i)): from the stored double reciprocal where the store has one
+// (MathFast::div, exact for normal quotients), else divided.
+template <class CS, class M, class R>
+H9K_HD float div_npsi(M &m, float x, float npsi, R rget) {
+  if constexpr (CS::kRecip)
+    return m.div(x, npsi, rget());
+  else
+    return x / npsi;
+}
+
 // Runs visit(k) for k = 0, 1, ... while it returns true (the reference's
 // layer loops with EXIT).  The fast path (MathFast) unrolls two visits --
 // the second only if some lane needs it -- and hands a third to the exact
@@ -310,6 +342,7 @@ H9K_HD void cell_inv_pair(const G &g, const CS &cs) {
     const float pte = psi * ts / e;
     cs.set_lay(PF_PTE, i, pte);
     cs.set_lay(PF_C3, i, pte / (g.zi(i) - g.zi(i - 1)));
+    if constexpr (CS::kRecip) set_lay_d(cs, PF_RPSI0, i, recip64(-psi));
   }
   float mh = cs.lay(PF_HKS, 1);
   if (cs.lay(PF_HKS, 2) < mh) mh = cs.lay(PF_HKS, 2);
@@ -431,7 +464,10 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
             vol_eq = ts;
           } else {
             const float expo = one + OWN(PF_NINVB);
-            const float temp0 = m.powf((((-psi) + zwtmm - zlo) / (-psi)), expo);
+            auto rp = [&]() __attribute__((always_inline)) {
+              return join_d(OWN(PF_RPSI0), OWN(PF_RPSI1));
+            };
+            const float temp0 = m.powf(div_npsi<CS>(m, ((-psi) + zwtmm - zlo), -psi, rp), expo);
             if ((zwtmm < zhi) && (zwtmm > zlo)) {
               const float tempi = one;
               const float voleq1 = OWN(PF_PTE) / (zwtmm - zlo) * (tempi - temp0);
@@ -440,7 +476,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
               vol_eq = MINF(ts, vol_eq);
               vol_eq = MAXF(vol_eq, zero);
             } else {
-              const float tempi = m.powf(((-psi + zwtmm - zhi) / (-psi)), expo);
+              const float tempi = m.powf(div_npsi<CS>(m, (-psi + zwtmm - zhi), -psi, rp), expo);
               vol_eq = OWN(PF_C3) * (tempi - temp0);
               vol_eq = MAXF(vol_eq, 0.0f);
               vol_eq = MINF(ts, vol_eq);
@@ -460,7 +496,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
       [&](int h) __attribute__((always_inline)) -> FV<1> {
         const float npsi = -PSI(L);
         const float num = sel(h, aq ? (-PSI(L) + zwtmm - g.zi(L)) : npsi, zwtmm);
-        const float q = num / npsi;
+        const float q = div_npsi<CS>(m, num, npsi, [&]() { return lay_d(cs, PF_RPSI0, L); });
         const float ninv = LAYF(PF_NINVB, L);
         return FV<1>{{m.powf(sel(h, q, one + q), sel(h, one + ninv, ninv))}};
       },
@@ -632,8 +668,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // loops visit (usually one), at a runtime layer index; rous = s_y(L) of
   // the pre-update zwtmm came from the pair split above.
   auto s_y_at = [&](int i, float zmm) __attribute__((always_inline)) -> float {
-    return MAXF(cs.lay(PF_TS, i) * (one - m.powf((one + zmm / (-cs.lay(PF_PSI, i))), cs.lay(PF_NINVB, i))),
-                0.02f);
+    const float q = div_npsi<CS>(m, zmm, -cs.lay(PF_PSI, i), [&]() { return lay_d(cs, PF_RPSI0, i); });
+    return MAXF(cs.lay(PF_TS, i) * (one - m.powf((one + q), cs.lay(PF_NINVB, i))), 0.02f);
   };
   float rous = MAXF(TS(L) * (one - pY.v[0]), 0.02f);
   int jwt2 = jwt;
@@ -675,7 +711,10 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // :1015-1035 baseflow; s_y(L) for the new zwtmm (:1077-1080)
   zwtmm = 1000.0f * s.zwt;
   float rsub_top = 5.5E-3f * m.expf(-fff * s.zwt);
-  rous = MAXF(TS(L) * (one - m.powf((one + zwtmm / (-PSI(L))), LAYF(PF_NINVB, L))), 0.02f);
+  rous = MAXF(TS(L) * (one - m.powf((one + div_npsi<CS>(m, zwtmm, -PSI(L),
+                                                                [&]() { return lay_d(cs, PF_RPSI0, L); })),
+                                    LAYF(PF_NINVB, L))),
+              0.02f);
   // :1048-1118
   int jwt3 = jwt2;
   if (jwt2 == L) {

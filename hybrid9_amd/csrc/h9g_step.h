@@ -130,7 +130,7 @@ struct MathFast {
   h9m::Tabs T;
   bool special;
   H9K_HD float expf(float x) { return h9m::expf_nx(x, T, special); }
-  H9K_HD float powf(float x, float y) { return h9m::powf_nx(x, y, T, special); }
+  H9K_HD float powf(float x, float y) { return h9m::powf_nx<false>(x, y, T, special); }
   H9K_HD float div(float x, float, double r) {
     const float q = (float)((double)x * r);
     special |= is_subnormal(q);

@@ -90,3 +90,20 @@ def test_kernel_body_matches_oracle_random_cells(L, nisurf, grow):
     assert ref["rc"] == out["rc"] == 0
     assert same_bits(out["annual"], ref["annual"])
     assert same_bits(out["state"], refcase.pack_state(ref["state"], L))
+
+
+def test_kernel_body_degenerate_exponents():
+    """bsw = 1 makes 1-1/b zero (powf(x, 0) = 1 by glibc's special path,
+    which the fast powf without its y test must reproduce)."""
+    g = synth.land_cells()[5::997][:24]
+    p = synth.make_params(g, 8)
+    p["bsw"][::3, 2] = 1.0
+    p["bsw"][1::5, 6] = 1.0
+    f = synth.make_forcing(g, synth.cell_lat(g), synth.year_day0(1901), 365)
+    ref = port.run(zi=synth.ZI_L8, params=p, forcing=f, nisurf=24, year0=1901, nyears=1,
+                   grow_on=1, nthreads=8)
+    out = host_run(zi=synth.ZI_L8, params=p, forcing=f, nisurf=24, year0=1901, nyears=1,
+                   grow_on=1, state0=None, const_geo=1)
+    assert ref["rc"] == out["rc"]
+    assert same_bits(out["annual"], ref["annual"])
+    assert same_bits(out["state"], refcase.pack_state(ref["state"], 8))
