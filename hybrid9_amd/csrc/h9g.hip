@@ -73,6 +73,7 @@ struct KArgs {
   int *__restrict__ err;           // 4 rows x ncell: code, day, substep, value bits
   int *__restrict__ err_flag;
   unsigned *__restrict__ stamps;   // H9G_STAMPS builds: 8 phase cycle sums per wave
+  float *__restrict__ sv;          // pair kernel: substep rollback, PairStore::GBLOCK bytes per workgroup
 };
 
 __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
@@ -87,8 +88,14 @@ __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
 // Pair kernel (h9g_pair.h): two lanes per soil column, the per-layer powers
 // split over the pair.  Same arguments, layouts and results as
 // h9g_year_kernel.
+// Waves per SIMD: 3 at L = 8 (168 VGPRs, 3 x 53 KB LDS per CU); 2 at L = 10,
+// where 168 VGPRs spill ~90 registers into the substep loop.
+template <int L>
+constexpr int pair_waves() { return L <= 8 ? 3 : 2; }
+
 template <int L, class G>
-__global__ void __launch_bounds__(64 * H9G_PWAVES) __attribute__((amdgpu_waves_per_eu(3, 3)))
+__global__ void __launch_bounds__(64 * H9G_PWAVES)
+    __attribute__((amdgpu_waves_per_eu(pair_waves<L>(), pair_waves<L>())))
 h9g_pair_kernel(const KArgs a, const G g) {
   typedef PairStore<L, H9G_PLANES> PS;
   __shared__ uint64_t s_e2[32];
@@ -105,7 +112,8 @@ h9g_pair_kernel(const KArgs a, const G g) {
   if (c >= a.ncell) return;          // both lanes of a pair leave together
   const int n = a.ncell;
 
-  PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1], (const lds_float *)s_zt};
+  PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1], (const lds_float *)s_zt,
+        a.sv + (size_t)blockIdx.x * (PS::GBLOCK / sizeof(float))};
   const Split2 sp{h};
   St<L> s;
 #pragma unroll
@@ -617,6 +625,8 @@ struct h9g_ctx {
   float soil_ms = 0.0f;           // device time of the last h9g_soil_layer
   int soil_slow = 0;              // cells of the last layer summed in the reference's order
   int *d_slow = nullptr;
+  float *d_sv = nullptr;          // pair kernel rollback blocks
+  size_t sv_bytes = 0;
   int kind = 1;        // 1: h9g_pair_kernel (default), 2: h9g_solo_kernel (H9G_KERNEL=solo)
 };
 
@@ -699,6 +709,7 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_forc);
   (void)hipFree(ctx->d_ann);
   (void)hipFree(ctx->d_err);
+  (void)hipFree(ctx->d_sv);
   (void)hipFree(ctx->d_errflag);
   (void)hipFree(ctx->d_diag);
   (void)hipFree(ctx->d_gid);
@@ -944,6 +955,19 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   a.err = ctx->d_err;
   a.err_flag = ctx->d_errflag;
   a.stamps = nullptr;
+  a.sv = nullptr;
+  if (ctx->kind != 2) {
+    const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
+    const size_t need = ((ctx->n + per_block - 1) / per_block) * 65536;
+    if (ctx->sv_bytes < need) {
+      (void)hipFree(ctx->d_sv);
+      ctx->d_sv = nullptr;
+      ctx->sv_bytes = 0;
+      HIPCHK(hipMalloc(&ctx->d_sv, need));
+      ctx->sv_bytes = need;
+    }
+    a.sv = ctx->d_sv;
+  }
 #if defined(H9G_STAMPS)
   if (!ctx->d_stamps) HIPCHK(hipMalloc(&ctx->d_stamps, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8)));
   HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8), ctx->sc));

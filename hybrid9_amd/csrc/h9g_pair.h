@@ -43,20 +43,22 @@ enum : int {
   PF_PTE,                              // psi*ts/(one-one/bsw)
   PF_C3,                               // pte/(zi(I)-zi(I-1))
   PF_ROOTR,                            // rootr_col(1..L)
-  PF_SVH2O, PF_SVSMP,                  // substep rollback
-  PF_RPSI0, PF_RPSI1,                  // 1/(-psi) in double (recip64): low, high word
-  PF_N                                 //   (stores with kRecip only)
+  PF_RPSI0, PF_RPSI1,                  // 1/(-psi), double (recip64) low, high word   (kRecip)
+  PF_RTS0, PF_RTS1,                    // 1/theta_s, double                           (kRts)
+  PF_SVH2O, PF_SVSMP,                  // substep rollback (sv_* of the store)
+  PF_N
 };
 // per-cell fields
 enum : int {
-  PS_FMAX = 0, PS_MH3, PS_TSDZ1, PS_SVZWT, PS_SVWA, PS_SVRNF, PS_SVERR, PS_DAY,
+  PS_FMAX = 0, PS_MH3, PS_TSDZ1, PS_DAY,
   PS_LAI = PS_DAY + D_N,               // plant state, parked over the substeps (pair kernel)
   PS_LAIL, PS_PM, PS_PFM, PS_PLEN, PS_RDEPTH,
+  PS_DR0,                              // day-constant reciprocals, DR_N doubles (kDayRecip)
+  PS_SVZWT = PS_DR0 + 2 * DR_N,        // substep rollback (sv_* of the store)
+  PS_SVWA, PS_SVRNF, PS_SVERR,
   PS_N
 };
-enum : int {
-  PS_N_NOPARK = PS_LAI                 // per-cell fields of a store that does not park
-};
+enum : int { SV_ZWT = 0, SV_WA, SV_RNF, SV_ERR };   // sv_sc fields
 
 template <int K>
 struct FV {
@@ -76,10 +78,25 @@ H9K_HD float pair_swap(float v) {
 #endif
 }
 
+// A double kept as two float fields (low word, high word).
+H9K_HD double join_d(float lo, float hi) {
+  return __builtin_bit_cast(double, (uint64_t)__builtin_bit_cast(uint32_t, hi) << 32 |
+                                        __builtin_bit_cast(uint32_t, lo));
+}
+H9K_HD float lo_d(double v) { return __builtin_bit_cast(float, (uint32_t)__builtin_bit_cast(uint64_t, v)); }
+H9K_HD float hi_d(double v) {
+  return __builtin_bit_cast(float, (uint32_t)(__builtin_bit_cast(uint64_t, v) >> 32));
+}
+
 // ------------------------------------------------------------------ stores
+// Every store has the same interface: lay/set_lay (per-layer field p of
+// layer i), sc/set_sc (per-cell field k), slot/set_slot (own layer t of a
+// pair lane), day/set_day, the day reciprocals day_r/set_day_r, and the
+// substep rollback sv_* (q = 0: h2osoi_liq, 1: smp; k = SV_*).  kRecip,
+// kRts, kDayRecip say which reciprocal fields it holds (LDS budget).
 template <int L>
 struct FlatStore {                     // host: one flat array per cell
-  static constexpr bool kRecip = true;
+  static constexpr bool kRecip = true, kRts = true, kDayRecip = true, kRtsHK = true;
   static constexpr int N = PF_N * L + PS_N;
   float *b;
   const float *zt;                     // zi(0..L+1), then zi(0..L+1)/1000
@@ -94,8 +111,18 @@ struct FlatStore {                     // host: one flat array per cell
   H9K_HD void launder() {}
   H9K_HD float day(int f) const { return sc(PS_DAY + f); }
   H9K_HD void set_day(int f, float v) const { set_sc(PS_DAY + f, v); }
+  H9K_HD double day_r(int k) const { return join_d(sc(PS_DR0 + 2 * k), sc(PS_DR0 + 2 * k + 1)); }
+  H9K_HD void set_day_r(int k, double v) const {
+    set_sc(PS_DR0 + 2 * k, lo_d(v));
+    set_sc(PS_DR0 + 2 * k + 1, hi_d(v));
+  }
   H9K_HD float root(int i) const { return lay(PF_ROOTR, i); }
   H9K_HD void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
+  H9K_HD float sv_lay(int q, int i) const { return lay(PF_SVH2O + q, i); }
+  H9K_HD void sv_set_lay(int q, int i, float v) const { set_lay(PF_SVH2O + q, i, v); }
+  H9K_HD float sv_sc(int k) const { return sc(PS_SVZWT + k); }
+  H9K_HD void sv_set_sc(int k, float v) const { set_sc(PS_SVZWT + k, v); }
+  H9K_HD void sv_sync() const {}
 };
 
 // Device: [row][S] LDS block per wave, S = lanes per wave.  Layer i of a
@@ -104,16 +131,26 @@ struct FlatStore {                     // host: one flat array per cell
 // is a static offset from the pair's even column.  Per-cell fields are
 // spread the same way over the two columns.  Both lanes of a pair store
 // identical values to the same address where they both write.
+//
+// The substep rollback lives in global memory (L2-resident: 76 B per
+// cell), in a per-workgroup block shaped like the LDS block: the byte
+// offset of a value is its LDS address, so every rollback store is
+// `global_store v_lds_address, s_block + imm` with no address arithmetic.
+// That leaves LDS room, within 3 workgroups per CU (76 rows per wave), for
+// the reciprocal fields: 1/(-psi) at any L, 1/theta_s and the day
+// reciprocals at L = 8 (76 rows; L = 10: 73 rows).
 template <int L, int S>
 struct PairStore {
   static constexpr int NT = L / 2;
-  // 3 workgroups per CU leave 76 rows per wave: the reciprocal rows fit at
-  // L = 8 (72 rows), not at L = 10 (75 rows without them)
-  static constexpr bool kRecip = L <= 8;
-  static constexpr int NPF = kRecip ? PF_N : PF_RPSI0;
-  static constexpr int ROWS = NPF * NT + (PS_N + 1) / 2;
+  static constexpr bool kRecip = true, kRts = true, kDayRecip = true;
+  static constexpr bool kRtsHK = L > 8;                     // 256-VGPR kernels (h9g.hip pair_waves)
+  static constexpr int NPF = kRts ? PF_SVH2O : PF_RTS0;     // per-layer fields in LDS
+  static constexpr int NPS = kDayRecip ? PS_SVZWT : PS_DR0; // per-cell fields in LDS
+  static constexpr int ROWS = NPF * NT + (NPS + 1) / 2;
+  static constexpr int GBLOCK = 65536;                      // bytes per workgroup (>= any LDS address)
   lds_float *self, *even;
   const lds_float *zt;                 // zi(0..L+1), then zi(0..L+1)/1000 (per block)
+  float *svw;                          // this workgroup's rollback block (global)
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
   __device__ __forceinline__ float lay(int p, int i) const {
@@ -135,27 +172,59 @@ struct PairStore {
   }
   __device__ __forceinline__ float day(int f) const { return sc(PS_DAY + f); }
   __device__ __forceinline__ void set_day(int f, float v) const { set_sc(PS_DAY + f, v); }
+  __device__ __forceinline__ double day_r(int k) const {
+    return join_d(sc(PS_DR0 + 2 * k), sc(PS_DR0 + 2 * k + 1));
+  }
+  __device__ __forceinline__ void set_day_r(int k, double v) const {
+    set_sc(PS_DR0 + 2 * k, lo_d(v));
+    set_sc(PS_DR0 + 2 * k + 1, hi_d(v));
+  }
   __device__ __forceinline__ float root(int i) const { return lay(PF_ROOTR, i); }
   __device__ __forceinline__ void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
+  // rollback: rows q*NT + t (layers), 2*NT + k/2 (scalars) of the global block
+  __device__ __forceinline__ float *gl(const lds_float *p, int off) const {
+    return (float *)((char *)svw + (uint32_t)(size_t)p) + off;
+  }
+  __device__ __forceinline__ void sv_set_slot(int q, int t, float v) const { *gl(self, (q * NT + t) * S) = v; }
+  __device__ __forceinline__ float sv_lay(int q, int i) const {
+    return *gl(even, (q * NT + ((i - 1) >> 1)) * S + ((i - 1) & 1));
+  }
+  __device__ __forceinline__ void sv_set_lay(int q, int i, float v) const {
+    *gl(even, (q * NT + ((i - 1) >> 1)) * S + ((i - 1) & 1)) = v;
+  }
+  __device__ __forceinline__ float sv_sc(int k) const { return *gl(even, (2 * NT + (k >> 1)) * S + (k & 1)); }
+  __device__ __forceinline__ void sv_set_sc(int k, float v) const {
+    *gl(even, (2 * NT + (k >> 1)) * S + (k & 1)) = v;
+  }
+  // before reading back what the wave stored (the exact re-run)
+  __device__ __forceinline__ void sv_sync() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+#endif
+  }
 };
 
 // Device, one lane per column ("solo"): column `lane` of a [row][64] block,
-// every field in the lane's own column.
+// every field in the lane's own column; no reciprocal fields, no parking
+// (1054 waves = 5 blocks/CU), rollback in LDS.
 template <int L>
 struct SoloStore {
-  static constexpr bool kRecip = false;
-  static constexpr int NPF = PF_RPSI0;
-  static constexpr int ROWS = NPF * L + PS_N_NOPARK;   // 1054 waves = 5 blocks/CU: no plant parking
+  static constexpr bool kRecip = false, kRts = false, kDayRecip = false, kRtsHK = false;
+  static constexpr int NPF = PF_RPSI0 + 2;           // TS..ROOTR, SVH2O, SVSMP
+  static constexpr int NPS = PS_LAI + 4;             // FMAX..DAY, SV*
+  static constexpr int ROWS = NPF * L + NPS;
   lds_float *b;
   const lds_float *zt;
+  H9K_HD static constexpr int pr(int p) { return p < PF_RPSI0 ? p : p - (PF_SVH2O - PF_RPSI0); }
+  H9K_HD static constexpr int kr(int k) { return k < PS_LAI ? k : k - (PS_SVZWT - PS_LAI); }
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
-  __device__ __forceinline__ float lay(int p, int i) const { return b[(p * L + i - 1) * 64]; }
-  __device__ __forceinline__ void set_lay(int p, int i, float v) const { b[(p * L + i - 1) * 64] = v; }
-  __device__ __forceinline__ float sc(int k) const { return b[(NPF * L + k) * 64]; }
-  __device__ __forceinline__ void set_sc(int k, float v) const { b[(NPF * L + k) * 64] = v; }
-  __device__ __forceinline__ float slot(int p, int t) const { return b[(p * L + 2 * t) * 64]; }
-  __device__ __forceinline__ void set_slot(int p, int t, float v) const { b[(p * L + 2 * t) * 64] = v; }
+  __device__ __forceinline__ float lay(int p, int i) const { return b[(pr(p) * L + i - 1) * 64]; }
+  __device__ __forceinline__ void set_lay(int p, int i, float v) const { b[(pr(p) * L + i - 1) * 64] = v; }
+  __device__ __forceinline__ float sc(int k) const { return b[(NPF * L + kr(k)) * 64]; }
+  __device__ __forceinline__ void set_sc(int k, float v) const { b[(NPF * L + kr(k)) * 64] = v; }
+  __device__ __forceinline__ float slot(int p, int t) const { return b[(pr(p) * L + 2 * t) * 64]; }
+  __device__ __forceinline__ void set_slot(int p, int t, float v) const { b[(pr(p) * L + 2 * t) * 64] = v; }
   __device__ __forceinline__ void launder() {
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+v"(b), "+v"(zt)::"memory");
@@ -163,8 +232,15 @@ struct SoloStore {
   }
   __device__ __forceinline__ float day(int f) const { return sc(PS_DAY + f); }
   __device__ __forceinline__ void set_day(int f, float v) const { set_sc(PS_DAY + f, v); }
+  __device__ __forceinline__ double day_r(int) const { return 0.0; }
+  __device__ __forceinline__ void set_day_r(int, double) const {}
   __device__ __forceinline__ float root(int i) const { return lay(PF_ROOTR, i); }
   __device__ __forceinline__ void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
+  __device__ __forceinline__ float sv_lay(int q, int i) const { return lay(PF_SVH2O + q, i); }
+  __device__ __forceinline__ void sv_set_lay(int q, int i, float v) const { set_lay(PF_SVH2O + q, i, v); }
+  __device__ __forceinline__ float sv_sc(int k) const { return sc(PS_SVZWT + k); }
+  __device__ __forceinline__ void sv_set_sc(int k, float v) const { set_sc(PS_SVZWT + k, v); }
+  __device__ __forceinline__ void sv_sync() const {}
 };
 
 // Phase profiler (tools: H9G_STAMPS build only).  NoProf compiles away.
@@ -264,38 +340,32 @@ struct Split2 {
 
 // Rollback copy of a per-layer state array (1-based v[1..L]).
 template <int L, class CS>
-H9K_HD void save_layers(const SplitAll &, const CS &cs, int p, const float *v) {
+H9K_HD void save_layers(const SplitAll &, const CS &cs, int q, const float *v) {
 #pragma unroll
-  for (int i = 1; i <= L; i++) cs.set_lay(p, i, v[i]);
+  for (int i = 1; i <= L; i++) cs.sv_set_lay(q, i, v[i]);
 }
 template <int L, class CS>
-H9K_HD void save_layers(const Split2 &sp, const CS &cs, int p, const float *v) {
+H9K_HD void save_layers(const Split2 &sp, const CS &cs, int q, const float *v) {
 #pragma unroll
-  for (int t = 0; t < L / 2; t++) cs.set_slot(p, t, sel(sp.h, v[2 * t + 1], v[2 * t + 2]));
+  for (int t = 0; t < L / 2; t++) cs.sv_set_slot(q, t, sel(sp.h, v[2 * t + 1], v[2 * t + 2]));
 }
 
-// A double kept as two per-layer float fields (p: low word, p+1: high).
-H9K_HD double join_d(float lo, float hi) {
-  return __builtin_bit_cast(double, (uint64_t)__builtin_bit_cast(uint32_t, hi) << 32 |
-                                        __builtin_bit_cast(uint32_t, lo));
-}
 template <class CS>
 H9K_HD void set_lay_d(const CS &cs, int p, int i, double v) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, v);
-  cs.set_lay(p, i, __builtin_bit_cast(float, (uint32_t)u));
-  cs.set_lay(p + 1, i, __builtin_bit_cast(float, (uint32_t)(u >> 32)));
+  cs.set_lay(p, i, lo_d(v));
+  cs.set_lay(p + 1, i, hi_d(v));
 }
 template <class CS>
 H9K_HD double lay_d(const CS &cs, int p, int i) { return join_d(cs.lay(p, i), cs.lay(p + 1, i)); }
 
-// x / (-psi(i)): from the stored double reciprocal where the store has one
-// (MathFast::div, exact for normal quotients), else divided.
-template <class CS, class M, class R>
-H9K_HD float div_npsi(M &m, float x, float npsi, R rget) {
-  if constexpr (CS::kRecip)
-    return m.div(x, npsi, rget());
+// x / d, from a stored double reciprocal of d when Use (MathFast::div,
+// exact for normal quotients; MathExact divides), else divided.
+template <bool Use, class M, class R>
+H9K_HD float divr(M &m, float x, float d, R rget) {
+  if constexpr (Use)
+    return m.div(x, d, rget());
   else
-    return x / npsi;
+    return x / d;
 }
 
 // Runs visit(k) for k = 0, 1, ... while it returns true (the reference's
@@ -343,6 +413,7 @@ H9K_HD void cell_inv_pair(const G &g, const CS &cs) {
     cs.set_lay(PF_PTE, i, pte);
     cs.set_lay(PF_C3, i, pte / (g.zi(i) - g.zi(i - 1)));
     if constexpr (CS::kRecip) set_lay_d(cs, PF_RPSI0, i, recip64(-psi));
+    if constexpr (CS::kRts) set_lay_d(cs, PF_RTS0, i, recip64(ts));
   }
   float mh = cs.lay(PF_HKS, 1);
   if (cs.lay(PF_HKS, 2) < mh) mh = cs.lay(PF_HKS, 2);
@@ -411,24 +482,29 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // :325-331
   float rss;
   if (theta[1] <= 0.15f)
-    rss = DC(D_LIT) * m.expf(0.3563f * 100.0f * (0.15f - theta[1]));
+    rss = (10.0f + DC(D_LIT1000)) * m.expf(0.3563f * 100.0f * (0.15f - theta[1]));
   else
-    rss = (10.0f + DC(D_LIT1000) * (1.0f - theta[1] / TS(1)));
+    rss = (10.0f + DC(D_LIT1000) * (1.0f - divr<CS::kRts>(m, theta[1], TS(1), [&]() { return lay_d(cs, PF_RTS0, 1); })));
   // :344-389
   const float desatdT = DC(D_DESAT), gamma = DC(D_GAMMA);
-  const float PMc = DC(D_NUMC) / (desatdT + gamma * (one + rsc / DC(D_RAARAC)));
-  const float PMs = DC(D_NUMS) / (desatdT + gamma * (one + rss / DC(D_RAARAS)));
-  const float Ra = DC(D_RA);
+  // x / (day constant k): from the stored day reciprocal where the store has them
+#define DDIV(x, F, K) divr<CS::kDayRecip>(m, (x), DC(F), [&]() { return cs.day_r(K); })
+  const float PMc = DC(D_NUMC) / (desatdT + gamma * (one + DDIV(rsc, D_RAARAC, DR_RAARAC)));
+  const float PMs = DC(D_NUMS) / (desatdT + gamma * (one + DDIV(rss, D_RAARAS, DR_RAARAS)));
+  const float Ra = DC(D_DG) * DC(D_RAA);
   const float Rs = DC(D_DGRAS) + gamma * rss;
   const float Rc = DC(D_DGRAC) + gamma * rsc;
   const float Cc = one / (one + Rc * Ra / (Rs * (Rc + Ra)));
   const float Cs = one / (one + Rs * Ra / (Rc * (Rs + Ra)));
   const float LE = Cc * PMc + Cs * PMs;
-  const float VDD0 = DC(D_VDD) + (DC(D_A1) - DC(D_DG) * LE) * DC(D_RAA) / DC(D_RHOCP);
-  const float LEc = (DC(D_DRR) + DC(D_RHOCP) * VDD0 / DC(D_RAC)) / (desatdT + gamma * (1.0f + rsc / DC(D_RAC)));
-  const float LEs = (DC(D_DRG) + DC(D_RHOCP) * VDD0 / DC(D_RAS)) / (desatdT + gamma * (1.0f + rss / DC(D_RAS)));
-  const float tran = LEc * 1.0E3f / DC(D_RL);
-  float evg = LEs * 1.0E3f / DC(D_RL);
+  const float VDD0 = DC(D_VDD) + DDIV((DC(D_A1) - DC(D_DG) * LE) * DC(D_RAA), D_RHOCP, DR_RHOCP);
+  const float LEc = (DC(D_DRR) + DDIV(DC(D_RHOCP) * VDD0, D_RAC, DR_RAC)) /
+                    (desatdT + gamma * (1.0f + DDIV(rsc, D_RAC, DR_RAC)));
+  const float LEs = (DC(D_DRG) + DDIV(DC(D_RHOCP) * VDD0, D_RAS, DR_RAS)) /
+                    (desatdT + gamma * (1.0f + DDIV(rss, D_RAS, DR_RAS)));
+  const float tran = DDIV(LEc * 1.0E3f, D_RL, DR_RL);
+  float evg = DDIV(LEs * 1.0E3f, D_RL, DR_RL);
+#undef DDIV
   // :396-400
   float em1 = m.div(g.dz(1) * (theta[1] - watmin), dt, g.rdt()) - tran * ROOT(1);
   em1 = MAXF(zero, em1);
@@ -467,7 +543,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
             auto rp = [&]() __attribute__((always_inline)) {
               return join_d(OWN(PF_RPSI0), OWN(PF_RPSI1));
             };
-            const float temp0 = m.powf(div_npsi<CS>(m, ((-psi) + zwtmm - zlo), -psi, rp), expo);
+            const float temp0 = m.powf(divr<CS::kRecip>(m, ((-psi) + zwtmm - zlo), -psi, rp), expo);
             if ((zwtmm < zhi) && (zwtmm > zlo)) {
               const float tempi = one;
               const float voleq1 = OWN(PF_PTE) / (zwtmm - zlo) * (tempi - temp0);
@@ -476,13 +552,14 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
               vol_eq = MINF(ts, vol_eq);
               vol_eq = MAXF(vol_eq, zero);
             } else {
-              const float tempi = m.powf(div_npsi<CS>(m, (-psi + zwtmm - zhi), -psi, rp), expo);
+              const float tempi = m.powf(divr<CS::kRecip>(m, (-psi + zwtmm - zhi), -psi, rp), expo);
               vol_eq = OWN(PF_C3) * (tempi - temp0);
               vol_eq = MAXF(vol_eq, 0.0f);
               vol_eq = MINF(ts, vol_eq);
             }
           }
-          float z = psi * m.powf(MAXF(vol_eq / ts, 0.01f), -OWN(PF_BSW));
+          const float qv = divr<CS::kRts>(m, vol_eq, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); });
+          float z = psi * m.powf(MAXF(qv, 0.01f), -OWN(PF_BSW));
           return FV<1>{{MAXF(smpmin, z)}};
         },
         out);
@@ -496,7 +573,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
       [&](int h) __attribute__((always_inline)) -> FV<1> {
         const float npsi = -PSI(L);
         const float num = sel(h, aq ? (-PSI(L) + zwtmm - g.zi(L)) : npsi, zwtmm);
-        const float q = div_npsi<CS>(m, num, npsi, [&]() { return lay_d(cs, PF_RPSI0, L); });
+        const float q = divr<CS::kRecip>(m, num, npsi, [&]() { return lay_d(cs, PF_RPSI0, L); });
         const float ninv = LAYF(PF_NINVB, L);
         return FV<1>{{m.powf(sel(h, q, one + q), sel(h, one + ninv, ninv))}};
       },
@@ -509,7 +586,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     ve = MINF(TS(L), ve);
     sp.template pick<2>(
         [&](int h) __attribute__((always_inline)) -> FV<2> {
-          const float q2 = sel(h, ve, theta[L]) / TS(L);
+          const float q2 = divr<CS::kRts>(m, sel(h, ve, theta[L]), TS(L), [&]() { return lay_d(cs, PF_RTS0, L); });
           float sn = MAXF(0.5f * (one + q2), 0.01f);
           sn = MINF(one, sn);
           float x = sel(h, MAXF(q2, 0.01f), sn);
@@ -544,7 +621,10 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           FV<4> r;
           r.v[0] = s1 * s2;
           r.v[1] = (2.0f * bsw + 3.0f) * s2 * OWN(PF_ITS);
-          float s_node = MAXF(th / ts, 0.01f);
+          // (from the reciprocal only with room to spare in VGPRs: +35 spilled
+          // VGPRs at 168, measured)
+          float s_node = MAXF(divr<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }),
+                              0.01f);
           s_node = MINF(one, s_node);
           float sm = OWN(PF_PSI) * m.powf(s_node, -bsw);
           sm = MAXF(smpmin, sm);
@@ -668,7 +748,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // loops visit (usually one), at a runtime layer index; rous = s_y(L) of
   // the pre-update zwtmm came from the pair split above.
   auto s_y_at = [&](int i, float zmm) __attribute__((always_inline)) -> float {
-    const float q = div_npsi<CS>(m, zmm, -cs.lay(PF_PSI, i), [&]() { return lay_d(cs, PF_RPSI0, i); });
+    const float q = divr<CS::kRecip>(m, zmm, -cs.lay(PF_PSI, i), [&]() { return lay_d(cs, PF_RPSI0, i); });
     return MAXF(cs.lay(PF_TS, i) * (one - m.powf((one + q), cs.lay(PF_NINVB, i))), 0.02f);
   };
   float rous = MAXF(TS(L) * (one - pY.v[0]), 0.02f);
@@ -711,7 +791,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // :1015-1035 baseflow; s_y(L) for the new zwtmm (:1077-1080)
   zwtmm = 1000.0f * s.zwt;
   float rsub_top = 5.5E-3f * m.expf(-fff * s.zwt);
-  rous = MAXF(TS(L) * (one - m.powf((one + div_npsi<CS>(m, zwtmm, -PSI(L),
+  rous = MAXF(TS(L) * (one - m.powf((one + divr<CS::kRecip>(m, zwtmm, -PSI(L),
                                                                 [&]() { return lay_d(cs, PF_RPSI0, L); })),
                                     LAYF(PF_NINVB, L))),
               0.02f);
@@ -827,15 +907,16 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
 // one lane computes every layer with the full glibc special-case logic.
 template <int L, class G, class CS>
 H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const double *l2) {
+  cs.sv_sync();
   St<L> s;
 #pragma unroll
   for (int i = 1; i <= L; i++) {
-    s.h2o[i] = cs.lay(PF_SVH2O, i);
-    s.smp[i] = cs.lay(PF_SVSMP, i);
+    s.h2o[i] = cs.sv_lay(0, i);
+    s.smp[i] = cs.sv_lay(1, i);
   }
-  s.zwt = cs.sc(PS_SVZWT);
-  s.wa = cs.sc(PS_SVWA);
-  float rnf = cs.sc(PS_SVRNF), errval = zero;
+  s.zwt = cs.sv_sc(SV_ZWT);
+  s.wa = cs.sv_sc(SV_WA);
+  float rnf = cs.sv_sc(SV_RNF), errval = zero;
   MathExact me{{e2, l2}};
   const SplitAll sa;
   NoProf np;
@@ -843,13 +924,14 @@ H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const dou
   cs.launder();
 #pragma unroll
   for (int i = 1; i <= L; i++) {
-    cs.set_lay(PF_SVH2O, i, s.h2o[i]);
-    cs.set_lay(PF_SVSMP, i, s.smp[i]);
+    cs.sv_set_lay(0, i, s.h2o[i]);
+    cs.sv_set_lay(1, i, s.smp[i]);
   }
-  cs.set_sc(PS_SVZWT, s.zwt);
-  cs.set_sc(PS_SVWA, s.wa);
-  cs.set_sc(PS_SVRNF, rnf);
-  cs.set_sc(PS_SVERR, errval);
+  cs.sv_set_sc(SV_ZWT, s.zwt);
+  cs.sv_set_sc(SV_WA, s.wa);
+  cs.sv_set_sc(SV_RNF, rnf);
+  cs.sv_set_sc(SV_ERR, errval);
+  cs.sv_sync();
   return code;
 }
 
@@ -859,11 +941,11 @@ template <int L, class G, class SP, class CS, class PR>
 H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_sum, float &errval,
                         const h9m::Tabs &T, PR &pr) {
   pr.mark(0);
-  save_layers<L>(sp, cs, PF_SVH2O, s.h2o);
-  save_layers<L>(sp, cs, PF_SVSMP, s.smp);
-  cs.set_sc(PS_SVZWT, s.zwt);
-  cs.set_sc(PS_SVWA, s.wa);
-  cs.set_sc(PS_SVRNF, rnf_sum);
+  save_layers<L>(sp, cs, 0, s.h2o);
+  save_layers<L>(sp, cs, 1, s.smp);
+  cs.sv_set_sc(SV_ZWT, s.zwt);
+  cs.sv_set_sc(SV_WA, s.wa);
+  cs.sv_set_sc(SV_RNF, rnf_sum);
   MathFast mf{T, false};
   int code = hydrology_pair<L, G, MathFast, SP, CS, PR>(g, cs, sp, s, rnf_sum, errval, mf, pr);
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
@@ -872,13 +954,13 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
     cs.launder();
 #pragma unroll
     for (int i = 1; i <= L; i++) {
-      s.h2o[i] = cs.lay(PF_SVH2O, i);
-      s.smp[i] = cs.lay(PF_SVSMP, i);
+      s.h2o[i] = cs.sv_lay(0, i);
+      s.smp[i] = cs.sv_lay(1, i);
     }
-    s.zwt = cs.sc(PS_SVZWT);
-    s.wa = cs.sc(PS_SVWA);
-    rnf_sum = cs.sc(PS_SVRNF);
-    errval = cs.sc(PS_SVERR);
+    s.zwt = cs.sv_sc(SV_ZWT);
+    s.wa = cs.sv_sc(SV_WA);
+    rnf_sum = cs.sv_sc(SV_RNF);
+    errval = cs.sv_sc(SV_ERR);
   }
   return code;
 }

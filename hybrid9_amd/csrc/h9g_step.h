@@ -85,18 +85,22 @@ H9K_HD bool any_lane(bool p) {
 }
 
 // ------------------------------------------------------------ math policies
-H9K_HD bool is_subnormal(float q) {
+// A fast-division quotient that must re-run exactly: subnormal (RN32 of the
+// double product may differ from the correctly rounded quotient there) or
+// NaN (recip64 of a zero, infinite or NaN divisor is NaN; x/0 is not).
+H9K_HD bool bad_quotient(float q) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_classf(q, 0x090);     // -denormal | +denormal
+  return __builtin_amdgcn_classf(q, 0x093);     // -denormal | +denormal | snan | qnan
 #else
   const uint32_t u = __builtin_bit_cast(uint32_t, q) & 0x7fffffffu;
-  return u != 0 && u < 0x00800000u;
+  return (u != 0 && u < 0x00800000u) || u > 0x7f800000u;
 #endif
 }
 
 // Reciprocal of a float divisor in double, |r - 1/d| <= 1.2 * 2^-53 |1/d|:
 // hardware estimate + two Newton steps (each squares the error and adds
-// <= 2^-53; two steps suffice from any estimate within 2^-14).
+// <= 2^-53; two steps suffice from any estimate within 2^-14).  NaN for
+// d = 0, inf or NaN (the Newton residual is 0 * inf).
 H9K_HD double recip64(float d) {
   const double dd = (double)d;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -117,7 +121,7 @@ H9K_HD double recip64(float d) {
 // a normal float: a float quotient that is not itself a rounding midpoint
 // lies at least 2^-49 (relative) away from every midpoint (x and d have
 // 24-bit significands), and a normal-range quotient is never exactly a
-// midpoint.  Subnormal results flag the substep for the exact re-run.
+// midpoint.  Subnormal and NaN results flag the substep for the exact re-run.
 struct MathExact {
   static constexpr bool kExact = true;
   h9m::Tabs T;
@@ -133,7 +137,7 @@ struct MathFast {
   H9K_HD float powf(float x, float y) { return h9m::powf_nx<false>(x, y, T, special); }
   H9K_HD float div(float x, float, double r) {
     const float q = (float)((double)x * r);
-    special |= is_subnormal(q);
+    special |= bad_quotient(q);
     return q;
   }
 };
@@ -143,10 +147,15 @@ struct MathFast {
 // stored per cell by day_consts through the store's set_day.
 enum : int {
   D_FORC = 0, D_DESAT, D_GAMMA, D_VDD, D_DG, D_RHOCP, D_A1, D_X, D_LAI2, D_PW28, D_RSCMIN,
-  D_RAC, D_RAA, D_RAS, D_RAARAC, D_RAARAS, D_NUMC, D_NUMS, D_RA, D_DGRAS, D_DGRAC, D_DRR,
-  D_DRG, D_RL, D_LIT, D_LIT1000, D_OK, D_N
+  D_RAC, D_RAA, D_RAS, D_RAARAC, D_RAARAS, D_NUMC, D_NUMS, D_DGRAS, D_DGRAC, D_DRR,
+  D_DRG, D_RL, D_LIT1000, D_OK, D_N
 };
-static_assert(D_N == 27, "day-constant block size");
+// (10 + 1000 LAI_litter and dg*raa are re-evaluated where used, from
+// D_LIT1000 and D_DG, D_RAA: same operations, one VALU each, one LDS row.)
+static_assert(D_N == 25, "day-constant block size");
+// Day constants that HYDROLOGY divides by, kept also as double reciprocals
+// (recip64) by stores with kDayRecip (exact fast division, h9g_pair.h).
+enum : int { DR_RAARAC = 0, DR_RAARAS, DR_RHOCP, DR_RAC, DR_RAS, DR_RL, DR_N };
 
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(3))) float lds_float;
@@ -213,7 +222,6 @@ H9K_HD void day_consts(const Day &d, float LAI, float LAI_litter, const CS &cs, 
   cs.set_day(D_RAA, raa);
   cs.set_day(D_RAS, ras);
   // :326-330 litter factors
-  cs.set_day(D_LIT, 10.0f + 1000.0f * LAI_litter);
   cs.set_day(D_LIT1000, 1000.0f * LAI_litter);
   // :335-389
   const float Rnet = d.Rnet;
@@ -231,12 +239,19 @@ H9K_HD void day_consts(const Day &d, float LAI, float LAI_litter, const CS &cs, 
   cs.set_day(D_NUMC, A1 + (rcv - desatdT * rac * (Rnets - G)) / raarac);
   cs.set_day(D_NUMS, A1 + (rcv - desatdT * ras * (Rnet - Rnets)) / raaras);
   cs.set_day(D_DG, dg);
-  cs.set_day(D_RA, dg * raa);
   cs.set_day(D_DGRAS, dg * ras);
   cs.set_day(D_DGRAC, dg * rac);
   cs.set_day(D_DRR, desatdT * (Rnet - Rnets));
   cs.set_day(D_DRG, desatdT * (Rnets - G));
   cs.set_day(D_RL, rhow * d.lamb);
+  if constexpr (CS::kDayRecip) {
+    cs.set_day_r(DR_RAARAC, recip64(raarac));
+    cs.set_day_r(DR_RAARAS, recip64(raaras));
+    cs.set_day_r(DR_RHOCP, recip64(rhocp));
+    cs.set_day_r(DR_RAC, recip64(rac));
+    cs.set_day_r(DR_RAS, recip64(ras));
+    cs.set_day_r(DR_RL, recip64(rhow * d.lamb));
+  }
 }
 
 // GROW.f90:55-201 (nplants = 1, iGPT = 1).  rootr(L+1) is zeroed by the

@@ -94,3 +94,19 @@ def test_device_fast_division_is_correctly_rounded():
     assert np.array_equal(flag.astype(bool), sub | ((out != 0) & (np.abs(out) < np.float32(2.0 ** -126))))
     keep = flag == 0
     assert same_bits(out[keep], ref[keep])
+
+
+@pytest.mark.gpu
+def test_device_fast_division_defers_on_zero_inf_nan_divisors():
+    """recip64 of 0, inf or NaN is NaN, so MathFast::div defers (the IEEE
+    quotient is inf, 0 or NaN there)."""
+    import ctypes as C
+    import hybrid9_amd as h
+    d = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 0.0, np.inf], np.float32)
+    x = np.array([1.5, -2.0, 3.0, 0.0, 1.0, 0.0, np.inf], np.float32)
+    out = np.empty_like(x)
+    flag = np.empty(x.size, np.int32)
+    rc = h.lib().h9g_div_selftest(0, x.size, h._fp(x), h._fp(d), h._fp(out),
+                                  flag.ctypes.data_as(C.POINTER(C.c_int)))
+    assert rc == 0
+    assert flag.all()
