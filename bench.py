@@ -38,6 +38,9 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "grid-cell-steps/sec at 0.5° global (1/2/4/8 GPUs) + achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 VALU instruction per
+# 4 cycles per SIMD (MI355X_MICROARCH.md: v_add/v_fma issue cost 4 cycles)
+VALU_PEAK_GIPS = 1024 * 2.4 / 4
 
 WORKLOADS = {
     # BASELINE.json configs[1]: the metric's config (fits one GPU)
@@ -232,6 +235,13 @@ def main():
     traffic = None
     if pmc and pmc.get("hbm_bytes_per_launch"):
         traffic = pmc["hbm_bytes_per_launch"] / launch_s / 1e9
+    valu = None
+    n_valu = ((pmc or {}).get("counters_per_launch") or {}).get("SQ_INSTS_VALU")
+    if n_valu:
+        # the kernel's actual bound: VALU issue
+        valu = {"achieved": n_valu / launch_s / 1e9, "peak": VALU_PEAK_GIPS,
+                "unit": "G wave-VALU-instructions/s", "frac": n_valu / launch_s / 1e9 / VALU_PEAK_GIPS,
+                "insts_per_launch": n_valu, "source": pmc.get("source")}
 
     out = {
         "metric": METRIC,
@@ -255,7 +265,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ctx.kernel_name(), "kernel_ms_per_launch": launch_s * 1e3,
                      "algorithmic_bytes_per_launch": algo_bytes_launch,
-                     "traffic_source": (pmc or {}).get("source")},
+                     "traffic_source": (pmc or {}).get("source"), "valu": valu},
         "cpu_baseline": None,
         "diagnostics_last_year": {k: float(v) for k, v in zip(h.DIAG_NAMES, diag)},
         "cells_stopped": failed,
