@@ -1029,6 +1029,13 @@ int h9g_sync(h9g_ctx *ctx) {
     fprintf(stderr, " total=%.0f\n", tot / steps);
   }
 #endif
+#if defined(H9G_COUNT_EXACT)
+  {
+    unsigned long long cnt = 0;
+    HIPCHK(hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(h9g_exact_count), sizeof(cnt)));
+    fprintf(stderr, "h9g exact re-runs (lanes, cumulative): %llu\n", cnt);
+  }
+#endif
   int flag = 0;
   HIPCHK(hipMemcpy(&flag, ctx->d_errflag, sizeof(int), hipMemcpyDeviceToHost));
   if (!flag) return 0;

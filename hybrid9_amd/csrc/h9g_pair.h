@@ -33,6 +33,9 @@
 #define __forceinline__ inline
 #endif
 
+#if defined(H9G_COUNT_EXACT)
+__device__ unsigned long long h9g_exact_count;   // exact re-runs (lanes), measurement builds only
+#endif
 namespace h9k {
 
 // per-layer store fields (L entries each)
@@ -949,6 +952,9 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
   MathFast mf{T, false};
   int code = hydrology_pair<L, G, MathFast, SP, CS, PR>(g, cs, sp, s, rnf_sum, errval, mf, pr);
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
+#if defined(H9G_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)
+    atomicAdd(&h9g_exact_count, 1ull);      // measurement builds only
+#endif
     cs.launder();
     code = substep_exact_pair<L, G, CS>(&g, cs, T.exp2, T.log2);
     cs.launder();
