@@ -56,12 +56,17 @@ enum : int {
   PS_FMAX = 0, PS_MH3, PS_TSDZ1, PS_DAY,
   PS_LAI = PS_DAY + D_N,               // plant state, parked over the substeps (pair kernel)
   PS_LAIL, PS_PM, PS_PFM, PS_PLEN, PS_RDEPTH,
-  PS_DR0,                              // day-constant reciprocals, DR_N doubles (kDayRecip)
+  PS_DR0,                              // day-constant reciprocals (kDayRecip): pairs
+  PS_DRS = PS_DR0 + 4 * DRP_N,         //   (c.lo s.lo c.hi s.hi), then shared doubles (lo hi)
   PS_SVZWT = PS_DR0 + 2 * DR_N,        // substep rollback (sv_* of the store)
   PS_SVWA, PS_SVRNF, PS_SVERR,
   PS_N
 };
 enum : int { SV_ZWT = 0, SV_WA, SV_RNF, SV_ERR };   // sv_sc fields
+// canopy/soil pairs share a row, canopy in the even column (see D_NUMC)
+static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_DAY + D_DGRAC) % 2 == 0 &&
+                  (PS_DAY + D_DRR) % 2 == 0 && (PS_DAY + D_RAC) % 2 == 0 && PS_DR0 % 2 == 0,
+              "pair fields must start a row");
 
 template <int K>
 struct FV {
@@ -114,10 +119,15 @@ struct FlatStore {                     // host: one flat array per cell
   H9K_HD void launder() {}
   H9K_HD float day(int f) const { return sc(PS_DAY + f); }
   H9K_HD void set_day(int f, float v) const { set_sc(PS_DAY + f, v); }
-  H9K_HD double day_r(int k) const { return join_d(sc(PS_DR0 + 2 * k), sc(PS_DR0 + 2 * k + 1)); }
+  H9K_HD double day_r(int k) const { return join_d(sc(PS_DRS + 2 * k), sc(PS_DRS + 2 * k + 1)); }
   H9K_HD void set_day_r(int k, double v) const {
-    set_sc(PS_DR0 + 2 * k, lo_d(v));
-    set_sc(PS_DR0 + 2 * k + 1, hi_d(v));
+    set_sc(PS_DRS + 2 * k, lo_d(v));
+    set_sc(PS_DRS + 2 * k + 1, hi_d(v));
+  }
+  H9K_HD double day_rp(int j, int h) const { return join_d(sc(PS_DR0 + 4 * j + h), sc(PS_DR0 + 4 * j + 2 + h)); }
+  H9K_HD void set_day_rp(int j, int h, double v) const {
+    set_sc(PS_DR0 + 4 * j + h, lo_d(v));
+    set_sc(PS_DR0 + 4 * j + 2 + h, hi_d(v));
   }
   H9K_HD float root(int i) const { return lay(PF_ROOTR, i); }
   H9K_HD void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
@@ -176,11 +186,24 @@ struct PairStore {
   __device__ __forceinline__ float day(int f) const { return sc(PS_DAY + f); }
   __device__ __forceinline__ void set_day(int f, float v) const { set_sc(PS_DAY + f, v); }
   __device__ __forceinline__ double day_r(int k) const {
-    return join_d(sc(PS_DR0 + 2 * k), sc(PS_DR0 + 2 * k + 1));
+    return join_d(sc(PS_DRS + 2 * k), sc(PS_DRS + 2 * k + 1));
   }
   __device__ __forceinline__ void set_day_r(int k, double v) const {
-    set_sc(PS_DR0 + 2 * k, lo_d(v));
-    set_sc(PS_DR0 + 2 * k + 1, hi_d(v));
+    set_sc(PS_DRS + 2 * k, lo_d(v));
+    set_sc(PS_DRS + 2 * k + 1, hi_d(v));
+  }
+  __device__ __forceinline__ double day_rp(int j, int h) const {
+    return join_d(sc(PS_DR0 + 4 * j + h), sc(PS_DR0 + 4 * j + 2 + h));
+  }
+  __device__ __forceinline__ void set_day_rp(int j, int h, double v) const {
+    set_sc(PS_DR0 + 4 * j + h, lo_d(v));
+    set_sc(PS_DR0 + 4 * j + 2 + h, hi_d(v));
+  }
+  // per-cell field k (even) + this lane's parity: the lane's own column of
+  // the row holding fields k, k+1
+  __device__ __forceinline__ float sc_own(int k) const { return self[(NPF * NT + (k >> 1)) * S]; }
+  __device__ __forceinline__ double day_rp_own(int j) const {
+    return join_d(sc_own(PS_DR0 + 4 * j), sc_own(PS_DR0 + 4 * j + 2));
   }
   __device__ __forceinline__ float root(int i) const { return lay(PF_ROOTR, i); }
   __device__ __forceinline__ void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
@@ -237,6 +260,8 @@ struct SoloStore {
   __device__ __forceinline__ void set_day(int f, float v) const { set_sc(PS_DAY + f, v); }
   __device__ __forceinline__ double day_r(int) const { return 0.0; }
   __device__ __forceinline__ void set_day_r(int, double) const {}
+  __device__ __forceinline__ double day_rp(int, int) const { return 0.0; }
+  __device__ __forceinline__ void set_day_rp(int, int, double) const {}
   __device__ __forceinline__ float root(int i) const { return lay(PF_ROOTR, i); }
   __device__ __forceinline__ void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
   __device__ __forceinline__ float sv_lay(int q, int i) const { return lay(PF_SVH2O + q, i); }
@@ -304,6 +329,11 @@ struct SplitAll {
     r1 = f(1);
   }
   H9K_HD bool pair_any(bool p) const { return p; }
+  // per-cell field k + h of a canopy/soil pair (k even), the pair's day reciprocal
+  template <class CS>
+  H9K_HD float own_sc(const CS &cs, int k, int h) const { return cs.sc(k + h); }
+  template <class CS>
+  H9K_HD double own_day_rp(const CS &cs, int j, int h) const { return cs.day_rp(j, h); }
 };
 
 // Two lanes per column (device fast path); h = lane & 1.
@@ -339,6 +369,10 @@ struct Split2 {
     const float f = p ? 1.0f : 0.0f;
     return (f + pair_swap(f)) != 0.0f;
   }
+  template <class CS>
+  H9K_HD float own_sc(const CS &cs, int k, int) const { return cs.sc_own(k); }
+  template <class CS>
+  H9K_HD double own_day_rp(const CS &cs, int j, int) const { return cs.day_rp_own(j); }
 };
 
 // Rollback copy of a per-layer state array (1-based v[1..L]).
@@ -488,26 +522,46 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     rss = (10.0f + DC(D_LIT1000)) * m.expf(0.3563f * 100.0f * (0.15f - theta[1]));
   else
     rss = (10.0f + DC(D_LIT1000) * (1.0f - divr<CS::kRts>(m, theta[1], TS(1), [&]() { return lay_d(cs, PF_RTS0, 1); })));
-  // :344-389
+  // :344-389.  The canopy (h = 0) and soil (h = 1) halves have the same
+  // expressions on different operands: each lane of a pair evaluates one
+  // (pick), reading its operands from its own column (D_NUMC comment).
   const float desatdT = DC(D_DESAT), gamma = DC(D_GAMMA);
-  // x / (day constant k): from the stored day reciprocal where the store has them
-#define DDIV(x, F, K) divr<CS::kDayRecip>(m, (x), DC(F), [&]() { return cs.day_r(K); })
-  const float PMc = DC(D_NUMC) / (desatdT + gamma * (one + DDIV(rsc, D_RAARAC, DR_RAARAC)));
-  const float PMs = DC(D_NUMS) / (desatdT + gamma * (one + DDIV(rss, D_RAARAS, DR_RAARAS)));
   const float Ra = DC(D_DG) * DC(D_RAA);
-  const float Rs = DC(D_DGRAS) + gamma * rss;
-  const float Rc = DC(D_DGRAC) + gamma * rsc;
-  const float Cc = one / (one + Rc * Ra / (Rs * (Rc + Ra)));
-  const float Cs = one / (one + Rs * Ra / (Rc * (Rs + Ra)));
-  const float LE = Cc * PMc + Cs * PMs;
-  const float VDD0 = DC(D_VDD) + DDIV((DC(D_A1) - DC(D_DG) * LE) * DC(D_RAA), D_RHOCP, DR_RHOCP);
-  const float LEc = (DC(D_DRR) + DDIV(DC(D_RHOCP) * VDD0, D_RAC, DR_RAC)) /
-                    (desatdT + gamma * (1.0f + DDIV(rsc, D_RAC, DR_RAC)));
-  const float LEs = (DC(D_DRG) + DDIV(DC(D_RHOCP) * VDD0, D_RAS, DR_RAS)) /
-                    (desatdT + gamma * (1.0f + DDIV(rss, D_RAS, DR_RAS)));
-  const float tran = DDIV(LEc * 1.0E3f, D_RL, DR_RL);
-  float evg = DDIV(LEs * 1.0E3f, D_RL, DR_RL);
-#undef DDIV
+  FV<2> ebc, ebs;                                       // {PM, R}: canopy, soil
+  sp.template pick<2>(
+      [&](int h) __attribute__((always_inline)) -> FV<2> {
+        const float r = sel(h, rsc, rss);
+        const float q = divr<CS::kDayRecip>(m, r, sp.own_sc(cs, PS_DAY + D_RAARAC, h),
+                                            [&]() { return sp.own_day_rp(cs, DRP_RAARA, h); });
+        const float PM = sp.own_sc(cs, PS_DAY + D_NUMC, h) / (desatdT + gamma * (one + q));
+        const float R = sp.own_sc(cs, PS_DAY + D_DGRAC, h) + gamma * r;
+        return FV<2>{{PM, R}};
+      },
+      ebc, ebs);
+  const float PMc = ebc.v[0], Rc = ebc.v[1], PMs = ebs.v[0], Rs = ebs.v[1];
+  FV<1> ccf, csf;                                       // Cc, Cs
+  sp.template pick<1>(
+      [&](int h) __attribute__((always_inline)) -> FV<1> {
+        const float Rh = sel(h, Rc, Rs), Ro = sel(h, Rs, Rc);
+        return FV<1>{{one / (one + Rh * Ra / (Ro * (Rh + Ra)))}};
+      },
+      ccf, csf);
+  const float LE = ccf.v[0] * PMc + csf.v[0] * PMs;
+  const float VDD0 = DC(D_VDD) + divr<CS::kDayRecip>(m, (DC(D_A1) - DC(D_DG) * LE) * DC(D_RAA), DC(D_RHOCP),
+                                                     [&]() { return cs.day_r(DR_RHOCP); });
+  FV<1> ftr, fev;                                       // tran, evg
+  sp.template pick<1>(
+      [&](int h) __attribute__((always_inline)) -> FV<1> {
+        const float r = sel(h, rsc, rss);
+        const float d = sp.own_sc(cs, PS_DAY + D_RAC, h);
+        auto rr = [&]() __attribute__((always_inline)) { return sp.own_day_rp(cs, DRP_RA, h); };
+        const float LEh = (sp.own_sc(cs, PS_DAY + D_DRR, h) + divr<CS::kDayRecip>(m, DC(D_RHOCP) * VDD0, d, rr)) /
+                          (desatdT + gamma * (1.0f + divr<CS::kDayRecip>(m, r, d, rr)));
+        return FV<1>{{divr<CS::kDayRecip>(m, LEh * 1.0E3f, DC(D_RL), [&]() { return cs.day_r(DR_RL); })}};
+      },
+      ftr, fev);
+  const float tran = ftr.v[0];
+  float evg = fev.v[0];
   // :396-400
   float em1 = m.div(g.dz(1) * (theta[1] - watmin), dt, g.rdt()) - tran * ROOT(1);
   em1 = MAXF(zero, em1);

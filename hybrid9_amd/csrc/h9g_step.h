@@ -145,17 +145,26 @@ struct MathFast {
 // ------------------------------------------------------------ cell data
 // Day-constant fields (HYDROLOGY.f90:232-389 terms fixed within a day),
 // stored per cell by day_consts through the store's set_day.
+// The canopy/soil pairs (c, s) come first, c at odd D index: with the
+// per-cell fields starting at an odd offset (h9g_pair.h PS_DAY) each pair
+// shares one row of the pair store, c in the even lane's column, s in the
+// odd lane's, so the pair-split energy balance reads its half with no select.
 enum : int {
-  D_FORC = 0, D_DESAT, D_GAMMA, D_VDD, D_DG, D_RHOCP, D_A1, D_X, D_LAI2, D_PW28, D_RSCMIN,
-  D_RAC, D_RAA, D_RAS, D_RAARAC, D_RAARAS, D_NUMC, D_NUMS, D_DGRAS, D_DGRAC, D_DRR,
-  D_DRG, D_RL, D_LIT1000, D_OK, D_N
+  D_FORC = 0,
+  D_NUMC, D_NUMS, D_RAARAC, D_RAARAS, D_DGRAC, D_DGRAS, D_DRR, D_DRG, D_RAC, D_RAS,
+  D_DESAT, D_GAMMA, D_VDD, D_DG, D_RHOCP, D_A1, D_X, D_LAI2, D_PW28, D_RSCMIN,
+  D_RAA, D_RL, D_LIT1000, D_OK, D_N
 };
 // (10 + 1000 LAI_litter and dg*raa are re-evaluated where used, from
 // D_LIT1000 and D_DG, D_RAA: same operations, one VALU each, one LDS row.)
 static_assert(D_N == 25, "day-constant block size");
 // Day constants that HYDROLOGY divides by, kept also as double reciprocals
-// (recip64) by stores with kDayRecip (exact fast division, h9g_pair.h).
-enum : int { DR_RAARAC = 0, DR_RAARAS, DR_RHOCP, DR_RAC, DR_RAS, DR_RL, DR_N };
+// (recip64) by stores with kDayRecip (exact fast division, h9g_pair.h):
+// the canopy/soil pairs DRP_* (raa+rac | raa+ras, rac | ras; day_rp(j, h))
+// and the shared DR_* (day_r(k)).  2 * DR_N float fields.
+enum : int { DRP_RAARA = 0, DRP_RA, DRP_N };
+enum : int { DR_RHOCP = 0, DR_RL, DR_N1 };
+enum : int { DR_N = 2 * DRP_N + DR_N1 };
 
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(3))) float lds_float;
@@ -245,11 +254,11 @@ H9K_HD void day_consts(const Day &d, float LAI, float LAI_litter, const CS &cs, 
   cs.set_day(D_DRG, desatdT * (Rnets - G));
   cs.set_day(D_RL, rhow * d.lamb);
   if constexpr (CS::kDayRecip) {
-    cs.set_day_r(DR_RAARAC, recip64(raarac));
-    cs.set_day_r(DR_RAARAS, recip64(raaras));
+    cs.set_day_rp(DRP_RAARA, 0, recip64(raarac));
+    cs.set_day_rp(DRP_RAARA, 1, recip64(raaras));
+    cs.set_day_rp(DRP_RA, 0, recip64(rac));
+    cs.set_day_rp(DRP_RA, 1, recip64(ras));
     cs.set_day_r(DR_RHOCP, recip64(rhocp));
-    cs.set_day_r(DR_RAC, recip64(rac));
-    cs.set_day_r(DR_RAS, recip64(ras));
     cs.set_day_r(DR_RL, recip64(rhow * d.lamb));
   }
 }
