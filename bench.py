@@ -241,7 +241,8 @@ def main():
         # the kernel's actual bound: VALU issue
         valu = {"achieved": n_valu / launch_s / 1e9, "peak": VALU_PEAK_GIPS,
                 "unit": "G wave-VALU-instructions/s", "frac": n_valu / launch_s / 1e9 / VALU_PEAK_GIPS,
-                "insts_per_launch": n_valu, "source": pmc.get("source")}
+                "insts_per_launch": n_valu,
+                "source": "rocprofv3 --pmc SQ_INSTS_VALU, profiles/pmc_%s.json" % pmc.get("tag")}
 
     out = {
         "metric": METRIC,

@@ -16,8 +16,9 @@
 //     cell-day is the 7 forcing values (coalesced, cell-fastest) plus the
 //     annual sums (L2-resident): the SHARED-state contract of each substep
 //     (376 B at L=8) never leaves the CU.
-//   * h9g_solo_kernel<L, G> (H9G_KERNEL=solo): one lane per column, the
-//     same code with one lane doing every layer.
+//   * h9g_solo_kernel<L, G> (default at L = 10; H9G_KERNEL=solo|pair
+//     overrides): one lane per column, the same code with one lane doing
+//     every layer.
 //   * glibc-exact expf/powf (h9_math.h) read their 32+16-entry tables from
 //     LDS (per-lane indices, no scalar-cache serialisation).
 //   * no MFMA: nothing here is GEMM-shaped.
@@ -627,7 +628,7 @@ struct h9g_ctx {
   int *d_slow = nullptr;
   float *d_sv = nullptr;          // pair kernel rollback blocks
   size_t sv_bytes = 0;
-  int kind = 1;        // 1: h9g_pair_kernel (default), 2: h9g_solo_kernel (H9G_KERNEL=solo)
+  int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel (H9G_KERNEL=pair|solo; default by L)
 };
 
 #define HIPCHK(x)                                                              \
@@ -781,8 +782,15 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
        {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}},
       {{"h9g_solo_kernel<8,GeoR>", "h9g_solo_kernel<8,GeoC<8,24>>", "h9g_solo_kernel<8,GeoC<8,48>>"},
        {"h9g_solo_kernel<10,GeoR>", "h9g_solo_kernel<10,GeoC<10,24>>", "h9g_solo_kernel<10,GeoC<10,48>>"}}};
+  // default: the pair kernel at L = 8; the solo kernel at L = 10, where the
+  // pair kernel is held to 2 waves/SIMD (measured: config 5 693 vs 725 ms)
   const char *kenv = getenv("H9G_KERNEL");
-  ctx->kind = (kenv && strcmp(kenv, "solo") == 0) ? 2 : 1;
+  if (kenv && strcmp(kenv, "solo") == 0)
+    ctx->kind = 2;
+  else if (kenv && strcmp(kenv, "pair") == 0)
+    ctx->kind = 1;
+  else
+    ctx->kind = (L == 8) ? 1 : 2;
   const GeoKind gk = geo_kind(*cfg);
   ctx->kname = names[ctx->kind][L == 8 ? 0 : 1][gk == GEO_R ? 0 : (gk == GEO_C24 ? 1 : 2)];
   return ctx;

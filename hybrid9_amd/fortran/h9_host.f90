@@ -54,9 +54,9 @@ REAL(C_FLOAT) :: zc (H9G_LMAX)
 CHARACTER (LEN = 4) :: ydate
 
 ! --- case.nml of the harness (oracle/ref/h9ref_main.f90) -------------------
-INTEGER :: ncell, state_override, ntrace, trace_cells (64)
+INTEGER :: ncell, state_override, ntrace, trace_cells (64), lclim_mode
 NAMELIST /h9case/ ncell, NISURF, year0, nyears, grow_on, state_override, &
-                  ntrace, trace_cells
+                  ntrace, trace_cells, lclim_mode
 
 TYPE(h9g_config) :: cfg
 TYPE(C_PTR) :: ctx
@@ -117,10 +117,12 @@ END DO
 !----------------------------------------------------------------------!
 state_override = 0
 IF (TRIM (input_mode) == 'case') THEN
-  ncell = 0; ntrace = 0; trace_cells = 0
+  ncell = 0; ntrace = 0; trace_cells = 0; lclim_mode = 0
   OPEN (NEWUNIT = u, FILE = TRIM (case_dir)//'/case.nml', STATUS = 'OLD')
   READ (u, NML = h9case)
   CLOSE (u)
+  IF (lclim_mode /= 0) STOP 'h9_host: LCLIM cases run through h9g_run_site (hybrid9_amd.site)'
+
   nlayers = 8
   L = nlayers
   OPEN (NEWUNIT = u, FILE = TRIM (case_dir)//'/zi.f32', ACCESS = 'STREAM', &

@@ -110,10 +110,13 @@ def test_config2_full_grid_sampled_against_oracle():
     np.testing.assert_allclose(diag, hd, rtol=1e-12, atol=0)
 
 
-def test_config5_l10_quarter_degree_sample():
-    """10 soil layers (config 5) on 0.25 deg cells, NS=24, GROW on.  The
-    reference is compiled for 8 layers only (SHARED.f90:294), so L=10 parity
-    is against the oracle restatement (pinned at L=8 by the goldens)."""
+@pytest.mark.parametrize("kernel", ["pair", "solo"])
+def test_config5_l10_quarter_degree_sample(kernel, monkeypatch):
+    """10 soil layers (config 5) on 0.25 deg cells, NS=24, GROW on, both
+    year kernels (solo is the L=10 default).  The reference is compiled for 8
+    layers only (SHARED.f90:294), so L=10 parity is against the oracle
+    restatement (pinned at L=8 by the goldens)."""
+    monkeypatch.setenv("H9G_KERNEL", kernel)
     gid = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)[::97][:2048]
     ann, st, _ = _full_grid_gpu(gid, 10, 24, True, 1901, 1, nx=synth.NX025, ny=synth.NY025)
     ref = _oracle_sample(gid, np.arange(gid.size), 10, 24, 1, 1901, 1, synth.NX025, synth.NY025)
