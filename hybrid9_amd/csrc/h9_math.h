@@ -245,8 +245,9 @@ H9_HD float powf_nx(float x, float y, const Tabs &T, bool &special) {
   const uint32_t iy = asu32(y);
   const double logx = log2_inline(ix, T);
   const double ylogx = (double)y * logx;
-  special |= (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) | (CheckY && zeroinfnan(iy)) |
-             (((asu64(ylogx) >> 47) & 0xffff) >= (asu64(126.0) >> 47));
+  // (| on bools: evaluate every test, no branches)
+  special |= (int)(ix - 0x00800000u >= 0x7f800000u - 0x00800000u) | (int)(CheckY && zeroinfnan(iy)) |
+             (int)(((asu64(ylogx) >> 47) & 0xffff) >= (asu64(126.0) >> 47));
   return exp2_inline(ylogx, 0, T);
 }
 
