@@ -265,6 +265,8 @@ def main():
             s = host_fed.step(s)
         ctx.run_year(s, y)
         if world > 1:
+            # the previous year's all-reduce (torch's stream) is done with diag_t
+            torch.cuda.current_stream().synchronize()
             ctx.get_diagnostics(dev_ptr=diag_t.data_ptr())
             dist.all_reduce(diag_t)                # RCCL: global diagnostics only
             return None
