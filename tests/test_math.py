@@ -69,8 +69,9 @@ def div_inputs(n=1 << 22, seed=5):
     d[:k] = rng.uniform(-1e5, 1e5, k).astype(np.float32)
     d[k:2 * k] = np.ldexp(1.0 + rng.integers(-4, 5, k) * 2.0 ** -23,
                           rng.integers(-20, 20, k)).astype(np.float32)
-    x[2 * k:3 * k] = np.clip(d[2 * k:3 * k].astype(np.float64) * (1.0 + rng.uniform(-1e-6, 1e-6, k)),
-                             -3e38, 3e38).astype(np.float32)
+    with np.errstate(invalid="ignore"):     # NaN divisors here are filtered out below
+        x[2 * k:3 * k] = np.clip(d[2 * k:3 * k].astype(np.float64) * (1.0 + rng.uniform(-1e-6, 1e-6, k)),
+                                 -3e38, 3e38).astype(np.float32)
     x[3 * k:4 * k] = np.ldexp(rng.uniform(1, 2, k), rng.integers(-149, -100, k)).astype(np.float32)
     ok = np.isfinite(x) & np.isfinite(d) & (d != 0)
     return x[ok], d[ok]
