@@ -8,9 +8,10 @@ A *step* is one simulated calendar year for every land cell of the GPU:
 i.e. one ``h9g_run_year`` launch, followed by the per-year FP64 diagnostics
 that are all-reduced across GPUs over RCCL (torch.distributed "nccl").
 Inputs (soil parameters, a distinct forcing year per step) are generated on
-the device and resident in HBM before the timed region.  Weak scaling: each
-rank simulates the full synthetic 0.5 deg land grid with its own seed
-(SURVEY.md §8e).  Rank 0 prints one JSON line.
+the device and resident in HBM before the timed region.  Weak scaling (the
+default): each rank simulates the full synthetic land grid with its own seed;
+``--strong`` shards one fixed grid over the ranks instead.
+Rank 0 prints one JSON line.
 
 ``value`` = cell-steps/s over all ranks (cells x days x NISURF x K / max
 rank time).  ``roofline.achieved`` = the SURVEY.md §8d algorithmic bytes of
@@ -222,6 +223,9 @@ def main():
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: shard one fixed grid over the ranks (default: weak, "
+                         "a full grid per rank with seed + rank)")
     ap.add_argument("--host-fed", action="store_true",
                     help="PCIe-inclusive rate: every step's forcing year is copied from pinned host "
                          "memory (async, double-buffered); reported in DESIGN.md, never as `value`")
@@ -241,7 +245,18 @@ def main():
         gid = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)
         lat = synth.cell_lat(gid, synth.NX025, synth.NY025)
         zi = synth.ZI_L10
-    seed = (args.seed if args.seed is not None else synth.SEED) + rank   # weak scaling
+    n_total = gid.size
+    if args.strong:
+        # strong scaling: one fixed grid, contiguous balanced
+        # shards of the land-cell list; parameters and forcing are keyed by
+        # the global cell id, so the shards are exactly the unsharded cells
+        from hybrid9_amd.shard import shard_slice
+        sl = shard_slice(gid.size, rank, world)
+        gid, lat = gid[sl], lat[sl]
+        seed = args.seed if args.seed is not None else synth.SEED
+    else:
+        seed = (args.seed if args.seed is not None else synth.SEED) + rank   # weak scaling
+        n_total = world * gid.size
     K, W = args.steps, args.warmup
     years = [1901 + i for i in range(W + K)]
 
@@ -293,8 +308,8 @@ def main():
     # (diag is the all-reduced sum over ranks for N > 1)
     failed = int(round(float(diag[11]))) if diag is not None else 0
     steps_per_cell = sum(synth.days_in_year(y) * ns for y in years[W:])
-    cell_steps_rank = (gid.size - failed / world) * steps_per_cell
-    value = (world * gid.size - failed) * steps_per_cell / elapsed
+    cell_steps_rank = (n_total - failed) / world * steps_per_cell
+    value = (n_total - failed) * steps_per_cell / elapsed
     launch_s = kern_ms / 1e3 / K
     algo_bytes_launch = cell_steps_rank / K * bytes_per_cell_step(L)
     achieved = algo_bytes_launch / launch_s / 1e9
@@ -320,12 +335,14 @@ def main():
         "warmup": W,
         "ms_per_step": elapsed / K * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (hybrid9_amd.synth seed %d+rank, generated on device; PGF/BNU "
-                "datasets are not available offline)" % (synth.SEED if args.seed is None else args.seed),
+        "data": "synthetic (hybrid9_amd.synth seed %d%s, generated on device; PGF/BNU "
+                "datasets are not available offline)" % (synth.SEED if args.seed is None else args.seed,
+                                                         "" if args.strong else "+rank"),
         "config": {"workload": f"{args.workload}: {wl['desc']}", "cells_per_gpu": int(gid.size),
+                   "cells_total": int(n_total),
                    "nlayers": L, "nisurf": ns, "grow": wl["grow_on"],
                    "years_per_step": 1, "parallelism": f"dp{world} (cell shards, RCCL all-reduce "
                    "of FP64 diagnostics per year)"},

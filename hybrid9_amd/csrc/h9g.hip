@@ -16,9 +16,9 @@
 //     cell-day is the 7 forcing values (coalesced, cell-fastest) plus the
 //     annual sums (L2-resident): the SHARED-state contract of each substep
 //     (376 B at L=8) never leaves the CU.
-//   * h9g_solo_kernel<L, G> (default at L = 10; H9G_KERNEL=solo|pair
-//     overrides): one lane per column, the same code with one lane doing
-//     every layer.
+//   * h9g_solo_kernel<L, G> (at L = 10 chosen by column count, l10_kind;
+//     H9G_KERNEL=solo|pair overrides): one lane per column, the same code
+//     with one lane doing every layer.
 //   * glibc-exact expf/powf (h9_math.h) read their 32+16-entry tables from
 //     LDS (per-lane indices, no scalar-cache serialisation).
 //   * no MFMA: nothing here is GEMM-shaped.
@@ -729,6 +729,22 @@ void h9g_destroy(h9g_ctx *ctx) {
   delete ctx;
 }
 
+// Kernel for L = 10 (1: pair, 2: solo).  Both are bit-identical; they differ
+// in how n columns quantise into rounds of resident waves.  The solo kernel
+// (1-wave blocks, 1 wave/SIMD: 256 VGPRs + 100 AGPRs) packs 64 columns per
+// wave; the pair kernel (88-column blocks, 2 waves/SIMD by LDS) 22.  Time per
+// round measured on config 5 (270,000 columns, 1 GPU): solo 693 ms / 5,
+// pair 725 ms / 6.  The solo kernel wins at 0.25 deg on one GPU; the pair
+// kernel on the smaller strong-scaling shards (e.g. 33,750 columns at N = 8:
+// one round either way, 121 vs 139 ms).
+static int l10_kind(size_t n, int ncu) {
+  const size_t solo_blocks = (n + H9G_YBLOCK - 1) / H9G_YBLOCK;
+  const size_t pair_blocks = (n + H9G_PCPW * H9G_PWAVES - 1) / (H9G_PCPW * H9G_PWAVES);
+  const size_t rs = (solo_blocks + 4 * (size_t)ncu - 1) / (4 * (size_t)ncu);
+  const size_t rp = (pair_blocks + 2 * (size_t)ncu - 1) / (2 * (size_t)ncu);
+  return rs * 1386 <= rp * 1208 ? 2 : 1;
+}
+
 h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
   if (!cfg || cfg->ncell <= 0 || !(cfg->nlayers == 8 || cfg->nlayers == 10) || cfg->nisurf < 1 ||
       cfg->max_days < 366 || cfg->nslots < 1 || cfg->nslots > 8)
@@ -782,15 +798,21 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
        {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}},
       {{"h9g_solo_kernel<8,GeoR>", "h9g_solo_kernel<8,GeoC<8,24>>", "h9g_solo_kernel<8,GeoC<8,48>>"},
        {"h9g_solo_kernel<10,GeoR>", "h9g_solo_kernel<10,GeoC<10,24>>", "h9g_solo_kernel<10,GeoC<10,48>>"}}};
-  // default: the pair kernel at L = 8; the solo kernel at L = 10, where the
-  // pair kernel is held to 2 waves/SIMD (measured: config 5 693 vs 725 ms)
+  // default: the pair kernel at L = 8; at L = 10 the kernel that needs less
+  // time for this many columns (l10_kind)
   const char *kenv = getenv("H9G_KERNEL");
   if (kenv && strcmp(kenv, "solo") == 0)
     ctx->kind = 2;
   else if (kenv && strcmp(kenv, "pair") == 0)
     ctx->kind = 1;
-  else
-    ctx->kind = (L == 8) ? 1 : 2;
+  else if (L == 8)
+    ctx->kind = 1;
+  else {
+    int ncu = 256;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1)
+      ncu = 256;
+    ctx->kind = l10_kind(n, ncu);
+  }
   const GeoKind gk = geo_kind(*cfg);
   ctx->kname = names[ctx->kind][L == 8 ? 0 : 1][gk == GEO_R ? 0 : (gk == GEO_C24 ? 1 : 2)];
   return ctx;
