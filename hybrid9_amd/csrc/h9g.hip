@@ -16,9 +16,10 @@
 //     cell-day is the 7 forcing values (coalesced, cell-fastest) plus the
 //     annual sums (L2-resident): the SHARED-state contract of each substep
 //     (376 B at L=8) never leaves the CU.
-//   * h9g_solo_kernel<L, G> (at L = 10 chosen by column count, l10_kind;
-//     H9G_KERNEL=solo|pair overrides): one lane per column, the same code
-//     with one lane doing every layer.
+//   * h9g_solo_kernel<L, G> (at L = 10 chosen by column count, alone or
+//     followed by the pair kernel on the remainder, l10_kind;
+//     H9G_KERNEL=solo|pair|mixed overrides): one lane per column, the same
+//     code with one lane doing every layer.
 //   * glibc-exact expf/powf (h9_math.h) read their 32+16-entry tables from
 //     LDS (per-lane indices, no scalar-cache serialisation).
 //   * no MFMA: nothing here is GEMM-shaped.
@@ -62,7 +63,8 @@ static const double h_log2tab[32] = H9M_POWF_LOG2_TAB_INIT;
 // kernel arguments
 // ---------------------------------------------------------------------------
 struct KArgs {
-  int ncell;
+  int ncell;       // row stride of every per-cell array
+  int c0, cend;    // cells [c0, cend) of this launch
   int nt;          // days in the year
   int nisurf;
   int grow_on;
@@ -109,8 +111,8 @@ h9g_pair_kernel(const KArgs a, const G g) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane >= H9G_PLANES) return;
   const int h = lane & 1;
-  const int c = (blockIdx.x * H9G_PWAVES + wave) * H9G_PCPW + (lane >> 1);
-  if (c >= a.ncell) return;          // both lanes of a pair leave together
+  const int c = a.c0 + (blockIdx.x * H9G_PWAVES + wave) * H9G_PCPW + (lane >> 1);
+  if (c >= a.cend) return;           // both lanes of a pair leave together
   const int n = a.ncell;
 
   PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1], (const lds_float *)s_zt,
@@ -209,8 +211,8 @@ h9g_solo_kernel(const KArgs a, const G g) {
   if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.ncell) return;
+  const int c = a.c0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.cend) return;
   const int n = a.ncell;
   SS cs{(lds_float *)&s_cell[threadIdx.x], (const lds_float *)s_zt};
   const SplitAll sp;
@@ -628,7 +630,8 @@ struct h9g_ctx {
   int *d_slow = nullptr;
   float *d_sv = nullptr;          // pair kernel rollback blocks
   size_t sv_bytes = 0;
-  int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel (H9G_KERNEL=pair|solo; default by L)
+  int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel, 3: both (H9G_KERNEL=pair|solo|mixed; default by L)
+  size_t n_solo = 0;   // kind 3: cells [0, n_solo) run on the solo kernel, the rest on the pair kernel
 };
 
 #define HIPCHK(x)                                                              \
@@ -729,20 +732,29 @@ void h9g_destroy(h9g_ctx *ctx) {
   delete ctx;
 }
 
-// Kernel for L = 10 (1: pair, 2: solo).  Both are bit-identical; they differ
-// in how n columns quantise into rounds of resident waves.  The solo kernel
-// (1-wave blocks, 1 wave/SIMD: 256 VGPRs + 100 AGPRs) packs 64 columns per
-// wave; the pair kernel (88-column blocks, 2 waves/SIMD by LDS) 22.  Time per
-// round measured on config 5 (270,000 columns, 1 GPU): solo 693 ms / 5,
-// pair 725 ms / 6.  The solo kernel wins at 0.25 deg on one GPU; the pair
-// kernel on the smaller strong-scaling shards (e.g. 33,750 columns at N = 8:
-// one round either way, 121 vs 139 ms).
-static int l10_kind(size_t n, int ncu) {
-  const size_t solo_blocks = (n + H9G_YBLOCK - 1) / H9G_YBLOCK;
-  const size_t pair_blocks = (n + H9G_PCPW * H9G_PWAVES - 1) / (H9G_PCPW * H9G_PWAVES);
-  const size_t rs = (solo_blocks + 4 * (size_t)ncu - 1) / (4 * (size_t)ncu);
-  const size_t rp = (pair_blocks + 2 * (size_t)ncu - 1) / (2 * (size_t)ncu);
-  return rs * 1386 <= rp * 1208 ? 2 : 1;
+// Kernel for L = 10 (1: pair, 2: solo, 3: both).  They are bit-identical
+// and differ in how n columns quantise into rounds of resident waves.  The
+// solo kernel (1-wave blocks, 1 wave/SIMD: 256 VGPRs + 100 AGPRs) packs 64
+// columns per wave; the pair kernel (88-column blocks, 2 waves/SIMD by LDS)
+// 22.  Time per round measured on config 5 (270,000 columns, 1 GPU): solo
+// 693 ms / 5, pair 725 ms / 6.  Kind 3 runs the whole solo rounds and hands
+// the remainder (less than one solo round) to the pair kernel: at 0.25 deg
+// on one GPU that is 4 solo rounds + 1 pair round instead of 5 solo rounds.
+// Smaller strong-scaling shards take the pair kernel.  Returns the kind and
+// sets *n_solo (cells [0, n_solo) on the solo kernel, for kind 3).
+static int l10_kind(size_t n, int ncu, size_t *n_solo) {
+  const size_t per_pair = (size_t)H9G_PCPW * H9G_PWAVES, solo_round = (size_t)4 * ncu * H9G_YBLOCK;
+  auto pair_rounds = [&](size_t m) { return ((m + per_pair - 1) / per_pair + 2 * (size_t)ncu - 1) / (2 * (size_t)ncu); };
+  const size_t rs = (n + solo_round - 1) / solo_round;
+  const size_t t_solo = rs * 1386, t_pair = pair_rounds(n) * 1208;
+  const size_t full = n / solo_round;
+  const size_t t_mixed = full * 1386 + pair_rounds(n - full * solo_round) * 1208;
+  *n_solo = 0;
+  if (full >= 1 && n > full * solo_round && t_mixed < t_solo && t_mixed < t_pair) {
+    *n_solo = full * solo_round;
+    return 3;
+  }
+  return t_solo <= t_pair ? 2 : 1;
 }
 
 h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
@@ -792,27 +804,38 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     h9g_destroy(ctx);
     return nullptr;
   }
-  static const char *names[3][2][3] = {
+  static const char *names[4][2][3] = {
       {{"", "", ""}, {"", "", ""}},
       {{"h9g_pair_kernel<8,GeoR>", "h9g_pair_kernel<8,GeoC<8,24>>", "h9g_pair_kernel<8,GeoC<8,48>>"},
        {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}},
       {{"h9g_solo_kernel<8,GeoR>", "h9g_solo_kernel<8,GeoC<8,24>>", "h9g_solo_kernel<8,GeoC<8,48>>"},
-       {"h9g_solo_kernel<10,GeoR>", "h9g_solo_kernel<10,GeoC<10,24>>", "h9g_solo_kernel<10,GeoC<10,48>>"}}};
+       {"h9g_solo_kernel<10,GeoR>", "h9g_solo_kernel<10,GeoC<10,24>>", "h9g_solo_kernel<10,GeoC<10,48>>"}},
+      {{"h9g_solo_kernel<8,GeoR>+h9g_pair_kernel<8,GeoR>", "h9g_solo_kernel<8,GeoC<8,24>>+h9g_pair_kernel<8,GeoC<8,24>>",
+        "h9g_solo_kernel<8,GeoC<8,48>>+h9g_pair_kernel<8,GeoC<8,48>>"},
+       {"h9g_solo_kernel<10,GeoR>+h9g_pair_kernel<10,GeoR>",
+        "h9g_solo_kernel<10,GeoC<10,24>>+h9g_pair_kernel<10,GeoC<10,24>>",
+        "h9g_solo_kernel<10,GeoC<10,48>>+h9g_pair_kernel<10,GeoC<10,48>>"}}};
   // default: the pair kernel at L = 8; at L = 10 the kernel that needs less
   // time for this many columns (l10_kind)
   const char *kenv = getenv("H9G_KERNEL");
+  int ncu = 256;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1)
+    ncu = 256;
   if (kenv && strcmp(kenv, "solo") == 0)
     ctx->kind = 2;
   else if (kenv && strcmp(kenv, "pair") == 0)
     ctx->kind = 1;
-  else if (L == 8)
+  else if (kenv && strcmp(kenv, "mixed") == 0) {
+    // forced split (tests): H9G_SPLIT cells on the solo kernel, else the model's
+    ctx->kind = 3;
+    size_t ns = 0;
+    (void)l10_kind(n, ncu, &ns);
+    if (const char *sp = getenv("H9G_SPLIT")) ns = (size_t)strtoull(sp, nullptr, 10);
+    ctx->n_solo = std::min(ns, n);
+  } else if (L == 8)
     ctx->kind = 1;
-  else {
-    int ncu = 256;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1)
-      ncu = 256;
-    ctx->kind = l10_kind(n, ncu);
-  }
+  else
+    ctx->kind = l10_kind(n, ncu, &ctx->n_solo);
   const GeoKind gk = geo_kind(*cfg);
   ctx->kname = names[ctx->kind][L == 8 ? 0 : 1][gk == GEO_R ? 0 : (gk == GEO_C24 ? 1 : 2)];
   return ctx;
@@ -974,6 +997,8 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   HIPCHK(hipStreamWaitEvent(ctx->sc, ctx->ev_copied[slot], 0));
   KArgs a;
   a.ncell = (int)ctx->n;
+  a.c0 = 0;
+  a.cend = (int)ctx->n;
   a.nt = nt;
   a.nisurf = ctx->cfg.nisurf;
   a.grow_on = ctx->cfg.grow_on;
@@ -1018,6 +1043,22 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   if (ctx->kind == 2) {
     H9G_DISPATCH(ctx, h9g_solo_kernel, (unsigned)((ctx->n + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
                  ctx->sc, a);
+  } else if (ctx->kind == 3) {
+    // mixed (l10_kind): whole rounds of solo waves, then the pair kernel on the rest
+    const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
+    const size_t ns = ctx->n_solo;
+    if (ns > 0) {
+      a.c0 = 0;
+      a.cend = (int)ns;
+      H9G_DISPATCH(ctx, h9g_solo_kernel, (unsigned)((ns + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
+                   ctx->sc, a);
+    }
+    if (ns < ctx->n) {
+      a.c0 = (int)ns;
+      a.cend = (int)ctx->n;
+      H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n - ns + per_block - 1) / per_block), 64 * H9G_PWAVES,
+                   ctx->sc, a);
+    }
   } else {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n + per_block - 1) / per_block), 64 * H9G_PWAVES,

@@ -22,11 +22,13 @@ def _gpu_run(inp, L):
                  grow_on=bool(inp["grow_on"]), state0=inp["state0"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "solo"])
+@pytest.mark.parametrize("kernel", ["pair", "solo", "mixed"])
 @pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit")))
 def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
-    """Both year kernels (two lanes per column = the default; one lane)."""
+    """Both year kernels (two lanes per column = the default; one lane), and
+    both in one run (cells [0, 37) on the solo kernel, the rest on pair)."""
     monkeypatch.setenv("H9G_KERNEL", kernel)
+    monkeypatch.setenv("H9G_SPLIT", "37")
     meta, inp, exp = load_golden(name)
     out = _gpu_run(inp, meta["L"])
     assert out["rc"] == 0, out["err"]
@@ -110,13 +112,15 @@ def test_config2_full_grid_sampled_against_oracle():
     np.testing.assert_allclose(diag, hd, rtol=1e-12, atol=0)
 
 
-@pytest.mark.parametrize("kernel", ["pair", "solo"])
+@pytest.mark.parametrize("kernel", ["pair", "solo", "mixed"])
 def test_config5_l10_quarter_degree_sample(kernel, monkeypatch):
     """10 soil layers (config 5) on 0.25 deg cells, NS=24, GROW on, both
-    year kernels (solo is the L=10 default).  The reference is compiled for 8
-    layers only (SHARED.f90:294), so L=10 parity is against the oracle
-    restatement (pinned at L=8 by the goldens)."""
+    year kernels and the mixed launch (the L=10 choice follows the column
+    count, h9g.hip l10_kind).  The reference is compiled for 8 layers only
+    (SHARED.f90:294), so L=10 parity is against the oracle restatement
+    (pinned at L=8 by the goldens)."""
     monkeypatch.setenv("H9G_KERNEL", kernel)
+    monkeypatch.setenv("H9G_SPLIT", "1001")
     gid = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)[::97][:2048]
     ann, st, _ = _full_grid_gpu(gid, 10, 24, True, 1901, 1, nx=synth.NX025, ny=synth.NY025)
     ref = _oracle_sample(gid, np.arange(gid.size), 10, 24, 1, 1901, 1, synth.NX025, synth.NY025)
