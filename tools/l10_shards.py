@@ -26,7 +26,7 @@ def main():
         sl = shard_slice(gid.size, 0, world)
         g, la = gid[sl], lat[sl]
         row = [f"N={world} cells={g.size}"]
-        for k in ("pair", "solo", "auto"):
+        for k in ("pair", "solo", "mixed", "auto"):
             if k == "auto":
                 os.environ.pop("H9G_KERNEL", None)
             else:
