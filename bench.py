@@ -39,9 +39,17 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "grid-cell-steps/sec at 0.5° global (1/2/4/8 GPUs) + achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 VALU instruction per
-# 4 cycles per SIMD (MI355X_MICROARCH.md: v_add/v_fma issue cost 4 cycles)
-VALU_PEAK_GIPS = 1024 * 2.4 / 4
+# VALU issue peak: 1024 SIMDs x 2.4 GHz; a SIMD-32 takes a wave64 f32/i32
+# VALU instruction every 2 cycles when >= 2 waves interleave (one wave alone:
+# every 4), MI355X_MICROARCH.md constants table.  f64 arithmetic runs at half
+# that rate (78.6 vs 157.3 TF/s vector peak) and transcendentals at a
+# quarter, so a kernel's issue floor depends on its instruction mix:
+# VALU_CYCLES gives the SIMD cycles per wave64 instruction of each
+# rocprofv3 SQ_INSTS_VALU_* class; the rest of SQ_INSTS_VALU costs 2.
+VALU_PEAK_GIPS = 1024 * 2.4 / 2
+SIMD_HZ = 1024 * 2.4e9
+VALU_CYCLES = {"SQ_INSTS_VALU_ADD_F64": 4, "SQ_INSTS_VALU_MUL_F64": 4, "SQ_INSTS_VALU_FMA_F64": 4,
+               "SQ_INSTS_VALU_TRANS_F64": 8, "SQ_INSTS_VALU_TRANS_F32": 4, "SQ_INSTS_VALU_INT64": 4}
 
 WORKLOADS = {
     # BASELINE.json configs[1]: the metric's config (fits one GPU)
@@ -51,10 +59,20 @@ WORKLOADS = {
     "config3": dict(desc="0.5deg global synthetic land, 67,420 cells/GPU, NISURF=24, "
                          "HYDROLOGY+GROW coupled, L=8",
                     grid="05", nlayers=8, nisurf=24, grow_on=True),
+    # BASELINE.json configs[3]: the 30-year spin-up 1901-1930, state carried
+    # from year to year as HYBRID9.f90:93-130 carries it across its decade
+    # loop; every year's forcing is distinct and resident (30 x 691 MB).
+    # Default run: no warmup, the 30 years timed (`--steps` / `--warmup`
+    # override).  Weak scaling: 67,420 cells per GPU.
+    "config4": dict(desc="0.5deg global synthetic land, 67,420 cells/GPU, 30-year spin-up "
+                         "1901-1930, NISURF=48, HYDROLOGY+GROW, L=8",
+                    grid="05", nlayers=8, nisurf=48, grow_on=True, steps=30, warmup=0),
     "config5": dict(desc="0.25deg global synthetic land, 270,000 cells, 10 layers, NISURF=24, "
                          "GROW on",
                     grid="025", nlayers=10, nisurf=24, grow_on=True),
 }
+RING_MAX = 32                   # resident forcing years (a multiple of 4: leap-year period)
+SLOT_BUDGET = 120e9             # bytes of HBM the resident forcing years may take
 
 
 def bytes_per_cell_step(L: int) -> int:
@@ -94,39 +112,47 @@ def barrier_sync(ctx, torch, dist, world):
 
 
 def cpu_baseline(workload: dict, seed: int) -> dict:
-    """The reference (oracle/_ref/h9ref) on a bounded sample of the same
-    workload: P processes x C cells x 1 year, like `mpirun -np P` without MPI
-    (the reference's ranks never communicate during compute)."""
+    """The reference (oracle/_ref/h9ref, or h9ref_l10 for 10 layers) on a
+    bounded sample of the same workload: P processes x C cells x 1 year,
+    like `mpirun -np P` without MPI (the reference's ranks never
+    communicate during compute)."""
     from hybrid9_amd import synth
     from oracle import refcase
 
     P = int(os.environ.get("H9_CPU_PROCS", os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
     P = max(1, min(P, os.cpu_count() or 1, 64))
-    C = int(os.environ.get("H9_CPU_CELLS", "2048"))
     L, ns, grow = workload["nlayers"], workload["nisurf"], int(workload["grow_on"])
-    kind = "reference" if refcase.REF_BIN.exists() and L == 8 else "port"
-    land = synth.land_cells()
+    C = int(os.environ.get("H9_CPU_CELLS", "2048" if L == 8 else "1024"))
+    ref_bin = refcase.ref_bin(L)
+    kind = "reference" if ref_bin.exists() else "port"
+    if workload["grid"] == "05":
+        land, zi, lat_of = synth.land_cells(), synth.ZI_L8, (lambda g: synth.cell_lat(g))
+    else:
+        land = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)
+        zi, lat_of = synth.ZI_L10, (lambda g: synth.cell_lat(g, synth.NX025, synth.NY025))
+    assert zi.size == L + 2
     nt = synth.days_in_year(1901)
     tmp = Path(tempfile.mkdtemp(prefix="h9cpu_"))
     dirs = []
     for i in range(P):
         g = land[(i * 7919) % (land.size - C):][:C]
         p = synth.make_params(g, L, seed)
-        f = synth.make_forcing(g, synth.cell_lat(g), 0, nt, seed)
+        f = synth.make_forcing(g, lat_of(g), 0, nt, seed)
         d = tmp / f"p{i}"
-        refcase.write_case(d, zi=synth.ZI_L8, params=p, forcing=f, nisurf=ns, grow_on=grow)
+        if kind == "reference":
+            refcase.write_case(d, zi=zi, params=p, forcing=f, nisurf=ns, grow_on=grow)
         dirs.append((d, p, f))
     t0 = time.perf_counter()
     if kind == "reference":
-        procs = [subprocess.Popen([str(refcase.REF_BIN), str(d)], stdout=subprocess.PIPE,
+        procs = [subprocess.Popen([str(ref_bin), str(d)], stdout=subprocess.PIPE,
                                   stderr=subprocess.STDOUT) for d, _, _ in dirs]
         outs = [pr.communicate()[0].decode() for pr in procs]
         wall = time.perf_counter() - t0
         ok = all(pr.returncode == 0 and "STOP" not in o for pr, o in zip(procs, outs))
     else:
         from oracle import port
-        for d, p, f in dirs:
-            port.run(zi=synth.ZI_L8, params=p, forcing=f, nisurf=ns, grow_on=grow, nthreads=1)
+        for d, p, f in dirs[:1]:
+            port.run(zi=zi, params=p, forcing=f, nisurf=ns, grow_on=grow, nthreads=1)
         wall = time.perf_counter() - t0
         P = 1
         ok = True
@@ -134,8 +160,9 @@ def cpu_baseline(workload: dict, seed: int) -> dict:
     subprocess.run(["rm", "-rf", str(tmp)])
     return {"value": steps / wall, "unit": "cell-steps/s", "cores": P, "kind": kind,
             "sample": f"{'reference HYDROLOGY.f90 (amdflang -O2)' if kind == 'reference' else 'C port'}"
+                      f"{'' if L == 8 else ' rebuilt with nsoil_layers_max=10'}"
                       f" x {P} processes x {C} cells x 1 yr ({ns} substeps/day, GROW "
-                      f"{'on' if grow else 'off'}) = {steps:.3e} cell-steps in {wall:.1f} s"
+                      f"{'on' if grow else 'off'}, L={L}) = {steps:.3e} cell-steps in {wall:.1f} s"
                       f"{'' if ok else ' (a sample process STOPped)'}"}
 
 
@@ -155,6 +182,30 @@ def load_traffic(workload_name: str, kernel: str):
         if d.get("workload") == workload_name and norm(d.get("kernel", "")) == norm(kernel):
             best = d
     return best
+
+
+def valu_roofline(pmc, launch_s: float):
+    """The kernel's real bound, VALU issue, from the
+    rocprofv3 SQ counters of the same kernel and workload: `achieved` wave
+    instructions per second against the 2-cycle issue peak, and `floor_ms`
+    = the launch time if every SIMD issued the measured instruction mix at
+    its class costs (VALU_CYCLES) back to back; frac_of_mix = floor / time."""
+    cnt = (pmc or {}).get("counters_per_launch") or {}
+    n_valu = cnt.get("SQ_INSTS_VALU")
+    if not n_valu:
+        return None
+    out = {"achieved": n_valu / launch_s / 1e9, "peak": VALU_PEAK_GIPS,
+           "unit": "G wave-VALU-instructions/s", "frac": n_valu / launch_s / 1e9 / VALU_PEAK_GIPS,
+           "insts_per_launch": n_valu,
+           "source": "rocprofv3 --pmc SQ_INSTS_VALU*, profiles/pmc_%s.json" % pmc.get("tag")}
+    if all(k in cnt for k in VALU_CYCLES):
+        typed = sum(cnt[k] for k in VALU_CYCLES)
+        cyc = sum(cnt[k] * c for k, c in VALU_CYCLES.items()) + 2 * (n_valu - typed)
+        out["mix_cycles_per_launch"] = cyc
+        out["floor_ms"] = cyc / SIMD_HZ * 1e3
+        out["frac_of_mix"] = cyc / SIMD_HZ / launch_s
+        out["mix"] = {k: cnt[k] for k in VALU_CYCLES}
+    return out
 
 
 class HostFed:
@@ -193,14 +244,17 @@ class HostFed:
         self.k = 0
 
     def step(self, s):
-        """Year s of the run: its forcing goes to slot k % 2 (k-th call)."""
+        """Step s of the run (year 1901 + s): its forcing, host year
+        s % R (R = 4 or fewer source years, the leap-year period), goes to
+        slot k % 2 (k-th call); the next step's year is pushed behind it."""
+        R = len(self.arrs)
         slot = self.k % 2
         if self.k == 0 or self.k == self.W:       # first push of warmup / of the timed region
-            self.ctx.push_forcing(slot, self.arrs[s], async_=True)
-            self.bytes += self.arrs[s].nbytes
-        if s + 1 < len(self.arrs):                 # prefetch the next year behind this kernel
-            self.ctx.push_forcing(1 - slot, self.arrs[s + 1], async_=True)
-            self.bytes += self.arrs[s + 1].nbytes
+            self.ctx.push_forcing(slot, self.arrs[s % R], async_=True)
+            self.bytes += self.arrs[s % R].nbytes
+        if self.k + 1 != self.W:                   # prefetch the next year behind this kernel
+            self.ctx.push_forcing(1 - slot, self.arrs[(s + 1) % R], async_=True)
+            self.bytes += self.arrs[(s + 1) % R].nbytes
         self.k += 1
         return slot
 
@@ -215,27 +269,20 @@ class HostFed:
         self.bufs = []
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--seed", type=int, default=None)
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: shard one fixed grid over the ranks (default: weak, "
-                         "a full grid per rank with seed + rank)")
-    ap.add_argument("--host-fed", action="store_true",
-                    help="PCIe-inclusive rate: every step's forcing year is copied from pinned host "
-                         "memory (async, double-buffered); reported in DESIGN.md, never as `value`")
-    args = ap.parse_args()
+def plan(workload: str, W: int, K: int, world: int = 1, rank: int = 0, strong: bool = False,
+         seed: int | None = None) -> dict:
+    """Everything a rank's run is made of, decided on the host (no GPU):
+    its cells, the years of the W + K steps and the forcing ring.
 
-    rank, world, local, torch, dist = dist_setup(args.gpus)
-    import hybrid9_amd as h
+    Step s simulates calendar year 1901 + s.  Its forcing sits in slot
+    s % R of a ring of R = min(W + K, RING_MAX, HBM budget) resident
+    years, generated before the timed region; with R a multiple of 4 (or
+    every step its own slot) each slot's year has the same length as every
+    year that reuses it.  When W + K > R a later year re-reads the synthetic
+    forcing of the year R earlier (its state is different, so the work is
+    not repeated)."""
     from hybrid9_amd import synth
-
-    wl = WORKLOADS[args.workload]
+    wl = WORKLOADS[workload]
     L, ns = wl["nlayers"], wl["nisurf"]
     if wl["grid"] == "05":
         gid = synth.land_cells()
@@ -246,67 +293,152 @@ def main():
         lat = synth.cell_lat(gid, synth.NX025, synth.NY025)
         zi = synth.ZI_L10
     n_total = gid.size
-    if args.strong:
+    base = seed if seed is not None else synth.SEED
+    if strong:
         # strong scaling: one fixed grid, contiguous balanced
         # shards of the land-cell list; parameters and forcing are keyed by
         # the global cell id, so the shards are exactly the unsharded cells
         from hybrid9_amd.shard import shard_slice
         sl = shard_slice(gid.size, rank, world)
         gid, lat = gid[sl], lat[sl]
-        seed = args.seed if args.seed is not None else synth.SEED
+        rseed = base
     else:
-        seed = (args.seed if args.seed is not None else synth.SEED) + rank   # weak scaling
+        rseed = base + rank                       # weak scaling
         n_total = world * gid.size
-    K, W = args.steps, args.warmup
-    years = [1901 + i for i in range(W + K)]
+    nsteps = W + K
+    if nsteps < 1:
+        raise ValueError("--steps + --warmup must be >= 1")
+    slot_bytes = 7 * 366 * gid.size * 4
+    cap = max(4, min(RING_MAX, int(SLOT_BUDGET // slot_bytes)) // 4 * 4)
+    R = nsteps if nsteps <= cap else cap
+    years = [1901 + s for s in range(nsteps)]
+    slot_year = years[:R]
+    slot_of_step = [s % R for s in range(nsteps)]
+    for s, y in enumerate(years):
+        assert synth.days_in_year(slot_year[slot_of_step[s]]) == synth.days_in_year(y), (s, y)
+    return dict(workload=workload, wl=wl, L=L, ns=ns, grow_on=wl["grow_on"], zi=zi, gid=gid, lat=lat,
+                seed=rseed, n_total=n_total, years=years, nslots=R, slot_year=slot_year,
+                slot_of_step=slot_of_step, W=W, K=K)
 
-    ctx = h.Context(gid.size, zi, nlayers=L, nisurf=ns, grow_on=wl["grow_on"],
-                    nslots=W + K, device=local if world > 1 else 0)
+
+def make_exchange(ctx, torch, dist, world: int, device: str):
+    """The per-year cross-GPU step: this rank's FP64 diagnostics into a
+    device buffer, stream-ordered behind the year kernel with no host
+    synchronisation (h9g_get_diagnostics_async), then all-reduced (RCCL
+    over xGMI; gloo on CPU in the tests).  Returns (exchange, buffer)."""
+    import hybrid9_amd as h
+    if world <= 1:
+        return None, None
+    buf = torch.zeros(h.NDIAG, dtype=torch.float64, device=device)
+    on_gpu = device.startswith("cuda")
+
+    def exchange():
+        stream = torch.cuda.current_stream().cuda_stream if on_gpu else None
+        ctx.diagnostics_async(buf.data_ptr(), stream)
+        dist.all_reduce(buf)
+    return exchange, buf
+
+
+def timed_steps(ctx, pl: dict, exchange, sync) -> float:
+    """W untimed warmup years, then K timed years between two `sync`s
+    (barrier + device synchronisation).  Returns the elapsed seconds."""
+    W, K = pl["W"], pl["K"]
+    for s in range(W):
+        ctx.run_year(pl["slot_of_step"][s], pl["years"][s])
+        if exchange:
+            exchange()
+    sync()
+    ctx.total_kernel_ms(reset=True)
+    t0 = time.perf_counter()
+    for s in range(W, W + K):
+        ctx.run_year(pl["slot_of_step"][s], pl["years"][s])
+        if exchange:
+            exchange()
+    sync()
+    return time.perf_counter() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None, help="timed years (default 3; config4: 30)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed years (default 1; config4: 0)")
+    ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: shard one fixed grid over the ranks (default: weak, "
+                         "a full grid per rank with seed + rank)")
+    ap.add_argument("--host-fed", action="store_true",
+                    help="PCIe-inclusive rate: every step's forcing year is copied from pinned host "
+                         "memory (async, double-buffered); reported in DESIGN.md, never as `value`")
+    args = ap.parse_args()
+    wl = WORKLOADS[args.workload]
+    K = args.steps if args.steps is not None else wl.get("steps", 3)
+    W = args.warmup if args.warmup is not None else wl.get("warmup", 1)
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launched without torchrun: start one rank per GPU as child processes
+        # (no GPU has been touched in this process) and exit with their code
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+               f"--master-port={os.environ.get('MASTER_PORT', '29517')}", str(Path(__file__).resolve())]
+        raise SystemExit(subprocess.call(cmd + sys.argv[1:]))
+
+    rank, world, local, torch, dist = dist_setup(args.gpus)
+    import hybrid9_amd as h
+    from hybrid9_amd import synth
+
+    pl = plan(args.workload, W, K, world, rank, args.strong, args.seed)
+    L, ns, gid, lat = pl["L"], pl["ns"], pl["gid"], pl["lat"]
+    n_total, seed, years = pl["n_total"], pl["seed"], pl["years"]
+    host_fed = None
+    nslots = pl["nslots"]
+    if args.host_fed:
+        nslots = max(2, min(4, W + K))            # 2 push slots + up to 4 source years
+    ctx = h.Context(gid.size, pl["zi"], nlayers=L, nisurf=ns, grow_on=wl["grow_on"],
+                    nslots=nslots, device=local if world > 1 else 0)
     ctx.set_cells(gid, lat)
     ctx.synth_params(seed)
     ctx.init_state()
-    for s, y in enumerate(years):                  # forcing resident in HBM
-        ctx.synth_forcing(s, seed, synth.year_day0(y), synth.days_in_year(y))
+    src_years = pl["slot_year"] if not args.host_fed else years[:nslots]
+    for slot, y in enumerate(src_years):           # forcing resident in HBM
+        ctx.synth_forcing(slot, seed, synth.year_day0(y), synth.days_in_year(y))
     ctx.sync()
 
-    host_fed = HostFed(ctx, h, gid.size, years, W) if args.host_fed else None
+    if args.host_fed:
+        host_fed = HostFed(ctx, h, gid.size, src_years, W)
+        pl = dict(pl, slot_of_step=[None] * (W + K))
 
-    diag_t = None
-    if world > 1:
-        diag_t = torch.zeros(h.NDIAG, dtype=torch.float64, device=f"cuda:{local}")
+    device = f"cuda:{local}" if world > 1 else "cpu"
+    exchange, diag_t = make_exchange(ctx, torch, dist, world, device)
 
-    def step(s, y):
-        if host_fed is not None:
-            s = host_fed.step(s)
-        ctx.run_year(s, y)
-        if world > 1:
-            # the previous year's all-reduce (torch's stream) is done with diag_t
-            torch.cuda.current_stream().synchronize()
-            ctx.get_diagnostics(dev_ptr=diag_t.data_ptr())
-            dist.all_reduce(diag_t)                # RCCL: global diagnostics only
-            return None
-        return ctx.get_diagnostics()
+    class _Fed:                                      # --host-fed: push, then run
+        def __init__(self, c):
+            self.c = c
 
-    for s in range(W):
-        step(s, years[s])
-    barrier_sync(ctx, torch, dist, world)
-    ctx.total_kernel_ms(reset=True)
-    t0 = time.perf_counter()
-    diag = None
-    for k in range(K):
-        diag = step(W + k, years[W + k])
-    barrier_sync(ctx, torch, dist, world)
-    elapsed = time.perf_counter() - t0
+        def run_year(self, _slot, y):
+            self.c.run_year(host_fed.step(y - 1901), y)
+
+        def total_kernel_ms(self, reset=False):
+            return self.c.total_kernel_ms(reset)
+
+    def sync():
+        barrier_sync(ctx, torch, dist, world)
+
+    elapsed = timed_steps(_Fed(ctx) if host_fed else ctx, pl, exchange, sync)
     kern_ms = ctx.total_kernel_ms(reset=True)
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
         diag = diag_t.cpu().numpy()
+    else:
+        diag = ctx.get_diagnostics()
 
     # cells that hit a reference STOP stop computing: count only the others
     # (diag is the all-reduced sum over ranks for N > 1)
-    failed = int(round(float(diag[11]))) if diag is not None else 0
+    failed = int(round(float(diag[11])))
     steps_per_cell = sum(synth.days_in_year(y) * ns for y in years[W:])
     cell_steps_rank = (n_total - failed) / world * steps_per_cell
     value = (n_total - failed) * steps_per_cell / elapsed
@@ -317,14 +449,7 @@ def main():
     traffic = None
     if pmc and pmc.get("hbm_bytes_per_launch"):
         traffic = pmc["hbm_bytes_per_launch"] / launch_s / 1e9
-    valu = None
-    n_valu = ((pmc or {}).get("counters_per_launch") or {}).get("SQ_INSTS_VALU")
-    if n_valu:
-        # the kernel's actual bound: VALU issue
-        valu = {"achieved": n_valu / launch_s / 1e9, "peak": VALU_PEAK_GIPS,
-                "unit": "G wave-VALU-instructions/s", "frac": n_valu / launch_s / 1e9 / VALU_PEAK_GIPS,
-                "insts_per_launch": n_valu,
-                "source": "rocprofv3 --pmc SQ_INSTS_VALU, profiles/pmc_%s.json" % pmc.get("tag")}
+    valu = valu_roofline(pmc, launch_s)
 
     out = {
         "metric": METRIC,
@@ -344,7 +469,9 @@ def main():
         "config": {"workload": f"{args.workload}: {wl['desc']}", "cells_per_gpu": int(gid.size),
                    "cells_total": int(n_total),
                    "nlayers": L, "nisurf": ns, "grow": wl["grow_on"],
-                   "years_per_step": 1, "parallelism": f"dp{world} (cell shards, RCCL all-reduce "
+                   "years_per_step": 1, "years": f"{years[W]}-{years[-1]} timed",
+                   "forcing_slots": nslots,
+                   "parallelism": f"dp{world} (cell shards, RCCL all-reduce "
                    "of FP64 diagnostics per year)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -38,6 +38,7 @@ STOP_MESSAGES = {  # HYDROLOGY.f90 STOP sites
     4: "Problem in HYDROLOGY: Water imbalance > 0.1 mm",  # :1244-1274
 }
 LMAX = 10
+MAX_SLOTS = 512          # H9G_MAX_SLOTS
 
 
 class H9GError(RuntimeError):
@@ -85,6 +86,9 @@ def lib() -> C.CDLL:
         "h9g_abi_version": (C.c_int, []),
         "h9g_device_count": (C.c_int, []),
         "h9g_create": (vp, [C.POINTER(_Config), C.c_int]),
+        "h9g_create_error": (C.c_char_p, []),
+        "h9g_config_check": (C.c_int, [C.POINTER(_Config), C.c_char_p, C.c_int]),
+        "h9g_config_bytes": (C.c_size_t, [C.POINTER(_Config)]),
         "h9g_destroy": (None, [vp]),
         "h9g_set_params": (C.c_int, [vp, _FP, _FP, _FP, _FP, _FP]),
         "h9g_init_state": (C.c_int, [vp]),
@@ -101,6 +105,7 @@ def lib() -> C.CDLL:
         "h9g_last_error": (C.c_int, [vp, C.POINTER(_Error)]),
         "h9g_get_annual": (C.c_int, [vp, _FP]),
         "h9g_get_diagnostics": (C.c_int, [vp, _DP, vp]),
+        "h9g_get_diagnostics_async": (C.c_int, [vp, vp, vp]),
         "h9g_set_cells": (C.c_int, [vp, _I64P, _FP]),
         "h9g_synth_params": (C.c_int, [vp, C.c_uint64]),
         "h9g_synth_forcing": (C.c_int, [vp, C.c_int, C.c_uint64, C.c_int, C.c_int]),
@@ -169,6 +174,29 @@ def state_size(L: int) -> int:
     return 4 * L + 9
 
 
+def make_config(ncell: int, zi, *, nlayers: int = 8, nisurf: int = 48, grow_on: bool = True,
+                max_days: int = 366, nslots: int = 2) -> _Config:
+    """The ``h9g_config`` of a context, validated on the host by
+    ``h9g_config_check`` (no GPU needed); raises ValueError with its reason."""
+    zi = np.asarray(zi, dtype=np.float32)
+    if zi.size != nlayers + 2:
+        raise ValueError(f"zi must hold zi(0:L+1) = {nlayers + 2} values")
+    cfg = _Config()
+    cfg.ncell, cfg.nlayers, cfg.nisurf = int(ncell), int(nlayers), int(nisurf)
+    cfg.grow_on, cfg.max_days, cfg.nslots = int(bool(grow_on)), int(max_days), int(nslots)
+    for i, v in enumerate(zi):
+        cfg.zi[i] = float(v)
+    why = C.create_string_buffer(256)
+    if lib().h9g_config_check(C.byref(cfg), why, 256):
+        raise ValueError(f"invalid h9g_config: {why.value.decode()}")
+    return cfg
+
+
+def config_bytes(cfg: _Config) -> int:
+    """Device bytes a context of ``cfg`` allocates (h9g_config_bytes)."""
+    return int(lib().h9g_config_bytes(C.byref(cfg)))
+
+
 class Context:
     """One GPU, one shard of land cells (C-ABI ``h9g_ctx``)."""
 
@@ -179,11 +207,8 @@ class Context:
         zi = np.asarray(zi, dtype=np.float32)
         if zi.size != nlayers + 2:
             raise ValueError(f"zi must hold zi(0:L+1) = {nlayers + 2} values")
-        cfg = _Config()
-        cfg.ncell, cfg.nlayers, cfg.nisurf = int(ncell), int(nlayers), int(nisurf)
-        cfg.grow_on, cfg.max_days, cfg.nslots = int(bool(grow_on)), int(max_days), int(nslots)
-        for i, v in enumerate(zi):
-            cfg.zi[i] = float(v)
+        cfg = make_config(ncell, zi, nlayers=nlayers, nisurf=nisurf, grow_on=grow_on,
+                          max_days=max_days, nslots=nslots)
         self._lib = lb
         self.ncell, self.L, self.nisurf, self.grow_on = int(ncell), int(nlayers), int(nisurf), bool(grow_on)
         self.zi = zi
@@ -191,8 +216,9 @@ class Context:
         self._keep = {}
         self._h = lb.h9g_create(C.byref(cfg), int(device))
         if not self._h:
-            raise H9GError(f"h9g_create failed (ncell={ncell}, L={nlayers}, device={device}); "
-                           "is a gfx950 GPU visible?")
+            why = (lb.h9g_create_error() or b"").decode() or "unknown"
+            raise H9GError(f"h9g_create failed (ncell={ncell}, L={nlayers}, nslots={nslots}, "
+                           f"device={device}): {why}")
 
     # -- lifetime ---------------------------------------------------------
     def close(self):
@@ -348,6 +374,14 @@ class Context:
                                              C.c_void_p(dev_ptr) if dev_ptr else None),
                "h9g_get_diagnostics")
         return out
+
+    def diagnostics_async(self, dev_ptr: int, stream: int | None):
+        """Copy the diagnostics into device buffer dev_ptr, ordered on the
+        hipStream_t `stream` (e.g. torch's current stream before an RCCL
+        all-reduce) with no host synchronisation."""
+        _check(self._lib.h9g_get_diagnostics_async(self._h, C.c_void_p(dev_ptr),
+                                                   C.c_void_p(stream) if stream else None),
+               "h9g_get_diagnostics_async")
 
     def last_kernel_ms(self) -> float:
         return float(self._lib.h9g_last_kernel_ms(self._h))

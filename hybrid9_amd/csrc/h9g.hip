@@ -612,6 +612,7 @@ struct h9g_ctx {
   std::vector<int> slot_days;
   std::vector<hipEvent_t> ev_copied, ev_consumed;
   hipEvent_t ev0[NEVT], ev1[NEVT];
+  hipEvent_t ev_ext = nullptr, ev_diag = nullptr;   // h9g_get_diagnostics_async ordering
   int nev = 0;
   float last_ms = 0.0f;
   double total_ms = 0.0;
@@ -726,6 +727,8 @@ void h9g_destroy(h9g_ctx *ctx) {
     (void)hipEventDestroy(ctx->ev0[i]);
     (void)hipEventDestroy(ctx->ev1[i]);
   }
+  if (ctx->ev_ext) (void)hipEventDestroy(ctx->ev_ext);
+  if (ctx->ev_diag) (void)hipEventDestroy(ctx->ev_diag);
   for (auto p : ctx->h_pin) (void)hipHostFree(p);
   if (ctx->sc) hipStreamDestroy(ctx->sc);
   if (ctx->sx) hipStreamDestroy(ctx->sx);
@@ -757,13 +760,64 @@ static int l10_kind(size_t n, int ncu, size_t *n_solo) {
   return t_solo <= t_pair ? 2 : 1;
 }
 
-h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
-  if (!cfg || cfg->ncell <= 0 || !(cfg->nlayers == 8 || cfg->nlayers == 10) || cfg->nisurf < 1 ||
-      cfg->max_days < 366 || cfg->nslots < 1 || cfg->nslots > 8)
-    return nullptr;
+// Device bytes a context of this configuration allocates (h9g_create and
+// the pair kernel's per-workgroup rollback blocks).
+size_t h9g_config_bytes(const h9g_config *cfg) {
+  if (!cfg || cfg->ncell <= 0 || cfg->nlayers < 1 || cfg->max_days < 1 || cfg->nslots < 1) return 0;
+  const size_t n = (size_t)cfg->ncell, L = (size_t)cfg->nlayers;
+  const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
+  return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * (size_t)cfg->nslots +
+                          (12 + L) + 1) * n +
+         sizeof(int) * 4 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
+         ((n + per_block - 1) / per_block) * 65536;
+}
+
+static thread_local char g_create_reason[256];
+
+static int config_fail(char *reason, int len, const char *msg) {
+  if (reason && len > 0) snprintf(reason, (size_t)len, "%s", msg);
+  return H9G_EINVAL;
+}
+
+// Host-only validation of a configuration (no GPU needed): 0 or H9G_EINVAL
+// with a readable reason.  The slot count is bounded by memory, which
+// h9g_create checks against the device's free HBM.
+int h9g_config_check(const h9g_config *cfg, char *reason, int reason_len) {
+  if (reason && reason_len > 0) reason[0] = 0;
+  if (!cfg) return config_fail(reason, reason_len, "cfg is NULL");
+  if (cfg->ncell <= 0) return config_fail(reason, reason_len, "ncell must be > 0");
+  if (!(cfg->nlayers == 8 || cfg->nlayers == 10))
+    return config_fail(reason, reason_len, "nlayers must be 8 or 10");
+  if (cfg->nisurf < 1) return config_fail(reason, reason_len, "nisurf must be >= 1");
+  if (cfg->max_days < 366) return config_fail(reason, reason_len, "max_days must be >= 366");
+  if (cfg->nslots < 1 || cfg->nslots > H9G_MAX_SLOTS)
+    return config_fail(reason, reason_len, "nslots must be in [1, H9G_MAX_SLOTS]");
+  if ((size_t)cfg->ncell * 7 * (size_t)cfg->max_days > (size_t)INT32_MAX * 4)
+    return config_fail(reason, reason_len, "ncell * max_days too large for one slot");
   for (int i = 1; i <= cfg->nlayers + 1; i++)
-    if (!(cfg->zi[i] > cfg->zi[i - 1])) return nullptr;
-  if (hipSetDevice(device) != hipSuccess) return nullptr;
+    if (!(cfg->zi[i] > cfg->zi[i - 1])) return config_fail(reason, reason_len, "zi must increase strictly");
+  return 0;
+}
+
+const char *h9g_create_error(void) { return g_create_reason; }
+
+h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
+  g_create_reason[0] = 0;
+  if (h9g_config_check(cfg, g_create_reason, sizeof g_create_reason)) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) {
+    snprintf(g_create_reason, sizeof g_create_reason, "hipSetDevice(%d) failed: no gfx950 GPU visible?", device);
+    return nullptr;
+  }
+  {
+    size_t free_b = 0, total_b = 0;
+    const size_t need = h9g_config_bytes(cfg);
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && need > free_b) {
+      snprintf(g_create_reason, sizeof g_create_reason,
+               "needs %.2f GB of device memory, %.2f GB free (reduce nslots=%d)", need / 1e9, free_b / 1e9,
+               cfg->nslots);
+      return nullptr;
+    }
+  }
   h9g_ctx *ctx = new h9g_ctx();
   ctx->cfg = *cfg;
   ctx->device = device;
@@ -799,8 +853,13 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
          hipEventCreateWithFlags(&ctx->ev_consumed[s], hipEventDisableTiming) == hipSuccess;
   for (int i = 0; ok && i < NEVT; i++)
     ok = hipEventCreate(&ctx->ev0[i]) == hipSuccess && hipEventCreate(&ctx->ev1[i]) == hipSuccess;
+  if (ok)
+    ok = hipEventCreateWithFlags(&ctx->ev_ext, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&ctx->ev_diag, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
-    fprintf(stderr, "h9g_create: device allocation failed (ncell=%d)\n", cfg->ncell);
+    snprintf(g_create_reason, sizeof g_create_reason, "device allocation failed (ncell=%d, nslots=%d)",
+             cfg->ncell, cfg->nslots);
+    fprintf(stderr, "h9g_create: %s\n", g_create_reason);
     h9g_destroy(ctx);
     return nullptr;
   }
@@ -1193,6 +1252,23 @@ int h9g_get_diagnostics(h9g_ctx *ctx, double *host_out, double *dev_out) {
     HIPCHK(hipMemcpyAsync(dev_out, ctx->d_diag, sizeof(double) * H9G_NDIAG, hipMemcpyDeviceToDevice, ctx->sc));
   HIPCHK(hipStreamSynchronize(ctx->sc));
   if (host_out) HIPCHK(hipMemcpy(host_out, ctx->d_diag, sizeof(double) * H9G_NDIAG, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// Stream-ordered diagnostics hand-off for a cross-GPU all-reduce with no
+// host synchronisation: the copy into dev_out waits for the work already
+// queued on `stream` (e.g. last year's all-reduce still reading dev_out),
+// and `stream` waits for the copy.  The next h9g_run_year queues behind it
+// on the compute stream, so year k+1 runs while year k's all-reduce does.
+int h9g_get_diagnostics_async(h9g_ctx *ctx, double *dev_out, void *stream) {
+  if (!ctx || !dev_out) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipEventRecord(ctx->ev_ext, s));
+  HIPCHK(hipStreamWaitEvent(ctx->sc, ctx->ev_ext, 0));
+  HIPCHK(hipMemcpyAsync(dev_out, ctx->d_diag, sizeof(double) * H9G_NDIAG, hipMemcpyDeviceToDevice, ctx->sc));
+  HIPCHK(hipEventRecord(ctx->ev_diag, ctx->sc));
+  HIPCHK(hipStreamWaitEvent(s, ctx->ev_diag, 0));
   return 0;
 }
 

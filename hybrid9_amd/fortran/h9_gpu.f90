@@ -42,6 +42,22 @@ INTERFACE
     INTEGER(C_INT), VALUE :: device
     TYPE(C_PTR) :: h9g_create
   END FUNCTION
+  FUNCTION h9g_config_check (cfg, reason, reason_len) BIND(C, NAME='h9g_config_check')
+    IMPORT :: C_INT, C_CHAR, h9g_config
+    TYPE(h9g_config), INTENT(IN) :: cfg
+    CHARACTER(KIND=C_CHAR), INTENT(OUT) :: reason (*)
+    INTEGER(C_INT), VALUE :: reason_len
+    INTEGER(C_INT) :: h9g_config_check
+  END FUNCTION
+  FUNCTION h9g_config_bytes (cfg) BIND(C, NAME='h9g_config_bytes')
+    IMPORT :: C_SIZE_T, h9g_config
+    TYPE(h9g_config), INTENT(IN) :: cfg
+    INTEGER(C_SIZE_T) :: h9g_config_bytes
+  END FUNCTION
+  FUNCTION h9g_create_error () BIND(C, NAME='h9g_create_error')
+    IMPORT :: C_PTR
+    TYPE(C_PTR) :: h9g_create_error
+  END FUNCTION
   SUBROUTINE h9g_destroy (ctx) BIND(C, NAME='h9g_destroy')
     IMPORT :: C_PTR
     TYPE(C_PTR), VALUE :: ctx
@@ -134,6 +150,12 @@ INTERFACE
     TYPE(C_PTR), VALUE :: ctx, dev_out
     REAL(C_DOUBLE), INTENT(OUT) :: host_out (*)
     INTEGER(C_INT) :: h9g_get_diagnostics
+  END FUNCTION
+  FUNCTION h9g_get_diagnostics_async (ctx, dev_out, stream) &
+           BIND(C, NAME='h9g_get_diagnostics_async')
+    IMPORT :: C_PTR, C_INT
+    TYPE(C_PTR), VALUE :: ctx, dev_out, stream
+    INTEGER(C_INT) :: h9g_get_diagnostics_async
   END FUNCTION
   FUNCTION h9g_set_cells (ctx, gid, lat) BIND(C, NAME='h9g_set_cells')
     IMPORT :: C_PTR, C_INT, C_INT64_T, C_FLOAT

@@ -29,6 +29,7 @@
 #ifndef H9G_H
 #define H9G_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -40,6 +41,7 @@ extern "C" {
 #define H9G_NFORCING 7
 #define H9G_NANNUAL_SCALARS 11
 #define H9G_NDIAG 12
+#define H9G_MAX_SLOTS 512   /* forcing slots per context; HBM bounds it too */
 
 /* reference STOP sites (HYDROLOGY.f90) */
 #define H9G_ERR_TRIDIAG1 1   /* :806-812  bmx(1) == 0            */
@@ -60,7 +62,8 @@ typedef struct {
   int32_t nisurf;      /* substeps per day (driver.txt line 2, INIT.f90:183) */
   int32_t grow_on;     /* 1: CALL GROW daily (HYBRID9.f90:217); 0: frozen   */
   int32_t max_days;    /* forcing slot capacity in days (>= 366)            */
-  int32_t nslots;      /* forcing slots (2 = double-buffered prefetch)      */
+  int32_t nslots;      /* forcing slots (2 = double-buffered prefetch; up to
+                          H9G_MAX_SLOTS resident years, bounded by free HBM) */
   float zi[H9G_LMAX + 2]; /* zi(0:L+1) mm (driver.txt:17-26, INIT.f90:202)  */
 } h9g_config;
 
@@ -76,8 +79,16 @@ typedef struct {
 /* --- lifetime -------------------------------------------------------- */
 int h9g_abi_version(void);
 int h9g_device_count(void);
-/* Creates a context on HIP device `device`; NULL on failure. */
+/* Host-only validation of a configuration (needs no GPU): 0, or H9G_EINVAL
+ * with a NUL-terminated reason in `reason` (may be NULL). */
+int h9g_config_check(const h9g_config *cfg, char *reason, int reason_len);
+/* Device bytes a context of this configuration allocates (0 if invalid). */
+size_t h9g_config_bytes(const h9g_config *cfg);
+/* Creates a context on HIP device `device`; NULL on failure, with the
+ * reason (invalid field, free HBM short of h9g_config_bytes, no device)
+ * in h9g_create_error() of the calling thread. */
 h9g_ctx *h9g_create(const h9g_config *cfg, int device);
+const char *h9g_create_error(void);
 void h9g_destroy(h9g_ctx *ctx);
 
 /* --- parameters and state (INIT.f90) ---------------------------------- */
@@ -150,6 +161,11 @@ int h9g_get_annual(h9g_ctx *ctx, float *annual);
  * for an all-reduce across GPUs.  dev_out (may be NULL) receives a
  * device-side copy; host_out (may be NULL) a host copy. */
 int h9g_get_diagnostics(h9g_ctx *ctx, double *host_out, double *dev_out);
+/* Stream-ordered variant, no host synchronisation: copies the diagnostics
+ * into device buffer dev_out after the work already queued on `stream` (a
+ * hipStream_t, NULL = legacy default stream), and makes `stream` wait for
+ * the copy -- e.g. the stream an RCCL all-reduce of dev_out runs on. */
+int h9g_get_diagnostics_async(h9g_ctx *ctx, double *dev_out, void *stream);
 
 /* --- synthetic inputs (hybrid9_amd/synth.py, bit-identical) ----------- */
 /* Cells are identified by their grid id (iy*nx+ix) and latitude. */

@@ -74,6 +74,8 @@ def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=1,
     L = params["theta_s"].shape[1]
     n = params["fmax"].size
     zi = np.ascontiguousarray(zi, dtype=np.float32)
+    if zi.size != L + 2:
+        raise ValueError(f"zi must hold zi(0:L+1) = {L + 2} values, got {zi.size}")
     pp = pack_params(params)
     fo = np.ascontiguousarray(forcing, dtype=np.float32)
     if state0 is None:

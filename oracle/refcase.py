@@ -24,6 +24,17 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 REF_BIN = HERE / "_ref" / "h9ref"
+REF_BIN_L10 = HERE / "_ref" / "h9ref_l10"     # nsoil_layers_max = 10 rebuild (make ref10)
+
+
+def ref_bin(L: int) -> Path:
+    """The reference harness built for L soil layers (8: as shipped;
+    10: the parameter-only rebuild of SHARED.f90:294,300)."""
+    if L == 8:
+        return REF_BIN
+    if L == 10:
+        return REF_BIN_L10
+    raise ValueError(f"no reference build for L={L}")
 
 ANNUAL_SCALARS = ("npp", "plant_mass", "rnf", "evap", "tas", "rlds", "rsds",
                   "huss", "ps", "pr", "rhs")
@@ -70,6 +81,8 @@ def write_case(d, *, zi, params, forcing=None, nisurf=48, year0=1901, nyears=1,
     d.mkdir(parents=True, exist_ok=True)
     ncell = params["fmax"].size
     L = params["theta_s"].shape[1]
+    if np.asarray(zi).size != L + 2:
+        raise ValueError(f"zi must hold zi(0:L+1) = {L + 2} values, got {np.asarray(zi).size}")
     tc = list(trace_cells) or [0]
     nml = ("&h9case\n"
            f" ncell={ncell}, NISURF={nisurf}, year0={year0}, nyears={nyears},\n"
@@ -120,10 +133,13 @@ def parse_stop(out: str) -> dict:
     return info
 
 
-def run_ref(d, timeout=3600):
-    if not REF_BIN.exists():
-        raise FileNotFoundError(f"{REF_BIN} missing: run `make -C oracle ref`")
-    r = subprocess.run([str(REF_BIN), str(d)], capture_output=True, text=True,
+def run_ref(d, timeout=3600, L=None):
+    if L is None:
+        L = np.fromfile(Path(d) / "zi.f32", dtype=np.float32).size - 2
+    b = ref_bin(L)
+    if not b.exists():
+        raise FileNotFoundError(f"{b} missing: run `make -C oracle ref ref10`")
+    r = subprocess.run([str(b), str(d)], capture_output=True, text=True,
                        timeout=timeout)
     if "Fortran STOP" in (r.stdout + r.stderr) or "Problem" in r.stdout:
         raise RefStop(r.stdout)
