@@ -77,6 +77,7 @@ struct KArgs {
   int *__restrict__ err_flag;
   unsigned *__restrict__ stamps;   // H9G_STAMPS builds: 8 phase cycle sums per wave
   float *__restrict__ sv;          // pair kernel: substep rollback, PairStore::GBLOCK bytes per workgroup
+  const int *__restrict__ perm;    // lane slot -> cell (h9g_sort_kernel), or null: identity
 };
 
 __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
@@ -111,8 +112,9 @@ h9g_pair_kernel(const KArgs a, const G g) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane >= H9G_PLANES) return;
   const int h = lane & 1;
-  const int c = a.c0 + (blockIdx.x * H9G_PWAVES + wave) * H9G_PCPW + (lane >> 1);
-  if (c >= a.cend) return;           // both lanes of a pair leave together
+  const int slot = a.c0 + (blockIdx.x * H9G_PWAVES + wave) * H9G_PCPW + (lane >> 1);
+  if (slot >= a.cend) return;        // both lanes of a pair leave together
+  const int c = a.perm ? a.perm[slot] : slot;
   const int n = a.ncell;
 
   PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1], (const lds_float *)s_zt,
@@ -211,8 +213,9 @@ h9g_solo_kernel(const KArgs a, const G g) {
   if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};
-  const int c = a.c0 + blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.cend) return;
+  const int slot = a.c0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= a.cend) return;
+  const int c = a.perm ? a.perm[slot] : slot;
   const int n = a.ncell;
   SS cs{(lds_float *)&s_cell[threadIdx.x], (const lds_float *)s_zt};
   const SplitAll sp;
@@ -279,6 +282,70 @@ h9g_solo_kernel(const KArgs a, const G g) {
     atomicOr(a.err_flag, 1);
 #pragma unroll
     for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + cw] = __builtin_nanf("");
+  }
+}
+
+// Cell order of the next year kernel: a stable counting sort of the cells
+// by the layer holding their water table (jwt, HYDROLOGY.f90:499-508, from
+// the current zwt), failed cells last.  Cells are independent, so the order
+// changes no result; it makes the 22 columns of a wave take the same
+// jwt-dependent branches (equilibrium-profile cases :517-567, recharge
+// :856-904, water-table and drainage loops :923-1118), which otherwise
+// diverge once water tables rise into the columns.  One block.
+template <int L, class G>
+__global__ void __launch_bounds__(1024) h9g_sort_kernel(int n, const float *__restrict__ st,
+                                                        const int *__restrict__ err, int *__restrict__ perm,
+                                                        const G g) {
+  constexpr int NK = L + 2;
+  __shared__ int cnt[NK][1024];
+  __shared__ int base[NK];
+  const int t = threadIdx.x;
+  const int per = (n + 1023) / 1024;
+  const int b = t * per, e = min(n, b + per);
+  float zim[L + 1];
+#pragma unroll
+  for (int i = 1; i <= L; i++) zim[i] = g.zim(i);
+  const float *zwt = st + (size_t)(4 * L + 1) * n;
+  auto key = [&](int c) -> int { return err[c] ? L + 1 : jwt_of<L>(zwt[c], zim); };
+  int loc[NK];
+#pragma unroll
+  for (int k = 0; k < NK; k++) loc[k] = 0;
+  for (int c = b; c < e; c++) {
+    const int k = key(c);
+#pragma unroll
+    for (int j = 0; j < NK; j++) loc[j] += (j == k);
+  }
+#pragma unroll
+  for (int k = 0; k < NK; k++) cnt[k][t] = loc[k];
+  __syncthreads();
+  if (t < NK) {                   // exclusive scan of each key's counts over the threads
+    int sum = 0;
+    for (int j = 0; j < 1024; j++) {
+      const int v = cnt[t][j];
+      cnt[t][j] = sum;
+      sum += v;
+    }
+    base[t] = sum;
+  }
+  __syncthreads();
+  if (t == 0) {
+    int sum = 0;
+    for (int k = 0; k < NK; k++) {
+      const int v = base[k];
+      base[k] = sum;
+      sum += v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NK; k++) loc[k] = base[k] + cnt[k][t];
+  for (int c = b; c < e; c++) {
+    const int k = key(c);
+    int pos = 0;
+#pragma unroll
+    for (int j = 0; j < NK; j++)
+      if (j == k) pos = loc[j]++;
+    perm[pos] = c;
   }
 }
 
@@ -630,6 +697,8 @@ struct h9g_ctx {
   int soil_slow = 0;              // cells of the last layer summed in the reference's order
   int *d_slow = nullptr;
   float *d_sv = nullptr;          // pair kernel rollback blocks
+  int *d_perm = nullptr;          // cell order of the year kernel (h9g_sort_kernel)
+  int sort = 1;                   // H9G_SORT=0: identity order
   size_t sv_bytes = 0;
   int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel, 3: both (H9G_KERNEL=pair|solo|mixed; default by L)
   size_t n_solo = 0;   // kind 3: cells [0, n_solo) run on the solo kernel, the rest on the pair kernel
@@ -721,6 +790,7 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_lat);
   (void)hipFree(ctx->d_stamps);
   (void)hipFree(ctx->d_slow);
+  (void)hipFree(ctx->d_perm);
   for (auto e : ctx->ev_copied) hipEventDestroy(e);
   for (auto e : ctx->ev_consumed) hipEventDestroy(e);
   for (int i = 0; i < NEVT; i++) {
@@ -768,7 +838,7 @@ size_t h9g_config_bytes(const h9g_config *cfg) {
   const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
   return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * (size_t)cfg->nslots +
                           (12 + L) + 1) * n +
-         sizeof(int) * 4 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
+         sizeof(int) * 5 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
          ((n + per_block - 1) / per_block) * 65536;
 }
 
@@ -835,7 +905,8 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
             hipMalloc(&ctx->d_errflag, sizeof(int)) == hipSuccess &&
             hipMalloc(&ctx->d_diag, sizeof(double) * H9G_NDIAG) == hipSuccess &&
             hipMalloc(&ctx->d_gid, sizeof(int64_t) * n) == hipSuccess &&
-            hipMalloc(&ctx->d_lat, sizeof(float) * n) == hipSuccess;
+            hipMalloc(&ctx->d_lat, sizeof(float) * n) == hipSuccess &&
+            hipMalloc(&ctx->d_perm, sizeof(int) * n) == hipSuccess;
   if (ok) {
     ok = hipMemset(ctx->d_err, 0, sizeof(int) * 4 * n) == hipSuccess &&
          hipMemset(ctx->d_errflag, 0, sizeof(int)) == hipSuccess &&
@@ -876,6 +947,7 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
         "h9g_solo_kernel<10,GeoC<10,48>>+h9g_pair_kernel<10,GeoC<10,48>>"}}};
   // default: the pair kernel at L = 8; at L = 10 the kernel that needs less
   // time for this many columns (l10_kind)
+  if (const char *se = getenv("H9G_SORT")) ctx->sort = atoi(se) != 0;
   const char *kenv = getenv("H9G_KERNEL");
   int ncu = 256;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1)
@@ -1070,6 +1142,12 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   a.err_flag = ctx->d_errflag;
   a.stamps = nullptr;
   a.sv = nullptr;
+  a.perm = nullptr;
+  if (ctx->sort) {
+    H9G_DISPATCH(ctx, h9g_sort_kernel, 1, 1024, ctx->sc, (int)ctx->n, ctx->d_st, ctx->d_err, ctx->d_perm);
+    HIPCHK(hipGetLastError());
+    a.perm = ctx->d_perm;
+  }
   if (ctx->kind != 2) {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     const size_t need = ((ctx->n + per_block - 1) / per_block) * 65536;

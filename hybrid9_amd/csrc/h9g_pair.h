@@ -156,7 +156,11 @@ template <int L, int S>
 struct PairStore {
   static constexpr int NT = L / 2;
   static constexpr bool kRecip = true, kRts = true, kDayRecip = true;
+#if defined(H9G_RTSHK)
+  static constexpr bool kRtsHK = true;
+#else
   static constexpr bool kRtsHK = L > 8;                     // 256-VGPR kernels (h9g.hip pair_waves)
+#endif
   static constexpr int NPF = kRts ? PF_SVH2O : PF_RTS0;     // per-layer fields in LDS
   static constexpr int NPS = kDayRecip ? PS_SVZWT : PS_DR0; // per-cell fields in LDS
   static constexpr int ROWS = NPF * NT + (NPS + 1) / 2;

@@ -50,15 +50,20 @@ constexpr float watmin = 0.01f;            // HYDROLOGY.f90:135
 constexpr float sla1 = 23.0E-3f;           // INIT.f90:154
 constexpr float log_0p1 = -0x1.26bb1cp+1f; // LOG(0.1) as folded by flang
 
+#if defined(H9G_FASTMINMAX) && defined(__HIP_DEVICE_COMPILE__)   // experiment: v_max/v_min
+H9K_HD float MAXF(float a, float b) { return __builtin_fmaxf(a, b); }
+H9K_HD float MINF(float a, float b) { return __builtin_fminf(a, b); }
+#else
 H9K_HD float MAXF(float a, float b) { return a > b ? a : b; }
 H9K_HD float MINF(float a, float b) { return a < b ? a : b; }
+#endif
 H9K_HD float absf(float a) { return __builtin_fabsf(a); }
 
 // Scheduling fence: stops the machine scheduler from interleaving the
 // unrolled per-layer bodies (each a few powf with double-precision
 // temporaries), which otherwise multiplies the live register set by L.
 H9K_HD void sched_fence() {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(H9G_NOFENCE)
   __builtin_amdgcn_sched_barrier(0);
 #endif
 }
