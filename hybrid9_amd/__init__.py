@@ -103,6 +103,7 @@ def lib() -> C.CDLL:
         "h9g_run_year": (C.c_int, [vp, C.c_int, C.c_int]),
         "h9g_sync": (C.c_int, [vp]),
         "h9g_last_error": (C.c_int, [vp, C.POINTER(_Error)]),
+        "h9g_get_errors": (C.c_int, [vp, C.POINTER(C.c_int32)]),
         "h9g_get_annual": (C.c_int, [vp, _FP]),
         "h9g_get_diagnostics": (C.c_int, [vp, _DP, vp]),
         "h9g_get_diagnostics_async": (C.c_int, [vp, vp, vp]),
@@ -363,6 +364,13 @@ class Context:
         return dict(code=e.code, cell=e.cell, year=e.year, day=e.day, substep=e.substep,
                     value=e.value)
 
+    def get_errors(self) -> dict:
+        """Every cell's STOP record: code (0: none), day, substep, value."""
+        rec = np.empty((4, self.ncell), dtype=np.int32)
+        _check(self._lib.h9g_get_errors(self._h, rec.ctypes.data_as(C.POINTER(C.c_int32))), "h9g_get_errors")
+        return dict(code=rec[0].copy(), day=rec[1].copy(), substep=rec[2].copy(),
+                    value=rec[3].view(np.float32).copy())
+
     def get_annual(self) -> np.ndarray:
         out = np.empty((12 + self.L, self.ncell), dtype=np.float32)
         _check(self._lib.h9g_get_annual(self._h, _fp(out)), "h9g_get_annual")
@@ -435,12 +443,15 @@ def write_axy_nc(path, annual, gid, zc, nx: int = 720, ny: int = 360):
 
 
 def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=True,
-        state0: np.ndarray | None = None, device=0):
+        state0: np.ndarray | None = None, device=0, stop_on_error=True):
     """Run ``nyears`` years from ``year0`` for every cell (HYBRID9.f90:120-290).
 
     Same contract as ``oracle.port.run`` / ``oracle.refcase.run_case``:
     forcing is (7, ndays_total, ncell); returns dict(annual (nyears, 12+L,
-    ncell), state (packed), rc, err)."""
+    ncell), state (packed), rc, err, errors).  A cell reaching one of the
+    reference's STOPs stops (NaN means); with stop_on_error the run ends
+    after that year, as the reference program would, else the other cells
+    go on.  ``errors`` holds every cell's STOP record (Context.get_errors)."""
     L = params["theta_s"].shape[1]
     n = params["fmax"].size
     with Context(n, zi, nlayers=L, nisurf=nisurf, grow_on=grow_on, device=device) as ctx:
@@ -460,5 +471,6 @@ def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=True,
             d0 += nt
             if rc:
                 err = ctx.last_error()
-                break
-        return dict(annual=ann, state=ctx.get_state(), rc=rc, err=err)
+                if stop_on_error:
+                    break
+        return dict(annual=ann, state=ctx.get_state(), rc=rc, err=err, errors=ctx.get_errors())

@@ -1309,6 +1309,16 @@ int h9g_run_site(h9g_ctx *ctx, int nday, const float *sub, const float *daily, c
   return rc;
 }
 
+// Per-cell STOP records of the runs since the last state (re)set: 4 rows of
+// ncell int32 -- code (0 = none), day, substep, bits of the float value.
+int h9g_get_errors(h9g_ctx *ctx, int32_t *rec) {
+  if (!ctx || !rec) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  HIPCHK(hipMemcpy(rec, ctx->d_err, sizeof(int32_t) * 4 * ctx->n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
 int h9g_last_error(h9g_ctx *ctx, h9g_error *err) {
   if (!ctx || !err) return H9G_EINVAL;
   *err = ctx->last_err;

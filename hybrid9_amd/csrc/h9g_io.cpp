@@ -13,18 +13,24 @@
 //     dimensions (latitude, longitude, layer_centre_depth), coordinate
 //     variables, variable names, units and NaN _FillValue.
 //
-// Format: netCDF "classic" (CDF-1) and 64-bit-offset (CDF-2) files, read
-// and written directly (the format is a big-endian header followed by
-// the variables' data; record variables are interleaved per record).  The
-// reference writes netCDF-4/HDF5 (NF90_NETCDF4, :93); no HDF5 or netCDF
-// library exists in this image, so output is CDF-2 with the identical
-// schema, readable by every netCDF tool (and scipy.io.netcdf_file), and
-// input is CDF-1/2 (PGF .nc4 converts with `nccopy -k 64-bit-offset`).
+// Formats.  Input: netCDF-4 (HDF5) files -- what PGF v2.1 ships and what
+// READ_NET_CDF_3DR.f90 opens -- read through the HDF5 C library (1.10, in
+// /opt/conda/lib of this image; loaded with dlopen on first use, so
+// libh9g.so has no link-time dependency on it), and netCDF "classic"
+// (CDF-1) and 64-bit-offset (CDF-2) files, read directly (a big-endian
+// header followed by the variables' data; record variables interleaved per
+// record).  There is no libnetcdf in the image.  Output: CDF-2 with the
+// reference's schema (the reference writes netCDF-4, NF90_NETCDF4 at
+// WRITE_NET_CDF_3DR.f90:93), readable by every netCDF tool and by
+// scipy.io.netcdf_file.
+#include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
 #include <cmath>
+#include <mutex>
+#include <type_traits>
 #include <string>
 #include <thread>
 #include <vector>
@@ -198,6 +204,162 @@ struct NcReader {
     return -1;
   }
 };
+
+// ------------------------------------------------------- netCDF-4 (HDF5)
+// A netCDF-4 file is an HDF5 file whose variables are datasets in the root
+// group and whose dimensions are HDF5 dimension scales.  Only the HDF5 C
+// API entry points below are used (1.10 ABI: hid_t is 64-bit).
+typedef int64_t hid_t_;
+typedef unsigned long long hsize_t_;
+
+struct H5Api {
+  bool ok = false;
+  int (*open)(void);
+  int (*eset_auto2)(hid_t_, void *, void *);
+  hid_t_ (*fopen)(const char *, unsigned, hid_t_);
+  int (*fclose)(hid_t_);
+  long (*lget_name_by_idx)(hid_t_, const char *, int, int, hsize_t_, char *, size_t, hid_t_);
+  int (*lexists)(hid_t_, const char *, hid_t_);
+  hid_t_ (*dopen2)(hid_t_, const char *, hid_t_);
+  int (*dclose)(hid_t_);
+  hid_t_ (*dget_space)(hid_t_);
+  hid_t_ (*dget_type)(hid_t_);
+  int (*tget_class)(hid_t_);
+  int (*tclose)(hid_t_);
+  int (*sget_simple_extent_ndims)(hid_t_);
+  int (*sget_simple_extent_dims)(hid_t_, hsize_t_ *, hsize_t_ *);
+  int (*sselect_hyperslab)(hid_t_, int, const hsize_t_ *, const hsize_t_ *, const hsize_t_ *, const hsize_t_ *);
+  hid_t_ (*screate_simple)(int, const hsize_t_ *, const hsize_t_ *);
+  int (*sclose)(hid_t_);
+  int (*dread)(hid_t_, hid_t_, hid_t_, hid_t_, hid_t_, void *);
+  hid_t_ *native_float;
+};
+
+const H5Api &h5() {
+  static H5Api a;
+  static std::once_flag once;
+  std::call_once(once, []() {
+    void *h = nullptr;
+    for (const char *lib : {"libhdf5.so.103", "libhdf5.so", "/opt/conda/lib/libhdf5.so.103", "/opt/conda/lib/libhdf5.so"})
+      if ((h = dlopen(lib, RTLD_NOW | RTLD_LOCAL))) break;
+    if (!h) return;
+    bool ok = true;
+    auto get = [&](auto &fp, const char *name) {
+      fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+      ok = ok && fp;
+    };
+    get(a.open, "H5open");
+    get(a.eset_auto2, "H5Eset_auto2");
+    get(a.fopen, "H5Fopen");
+    get(a.fclose, "H5Fclose");
+    get(a.lget_name_by_idx, "H5Lget_name_by_idx");
+    get(a.lexists, "H5Lexists");
+    get(a.dopen2, "H5Dopen2");
+    get(a.dclose, "H5Dclose");
+    get(a.dget_space, "H5Dget_space");
+    get(a.dget_type, "H5Dget_type");
+    get(a.tget_class, "H5Tget_class");
+    get(a.tclose, "H5Tclose");
+    get(a.sget_simple_extent_ndims, "H5Sget_simple_extent_ndims");
+    get(a.sget_simple_extent_dims, "H5Sget_simple_extent_dims");
+    get(a.sselect_hyperslab, "H5Sselect_hyperslab");
+    get(a.screate_simple, "H5Screate_simple");
+    get(a.sclose, "H5Sclose");
+    get(a.dread, "H5Dread");
+    a.native_float = (hid_t_ *)dlsym(h, "H5T_NATIVE_FLOAT_g");
+    ok = ok && a.native_float && a.open() >= 0;
+    if (ok) a.eset_auto2(0, nullptr, nullptr);     // H5E_DEFAULT: no error stack printing
+    a.ok = ok;
+  });
+  return a;
+}
+
+// HDF5 signature at offset 0 (or a user block of 512, 1024, 2048 bytes)
+bool is_hdf5(const char *path) {
+  static const unsigned char sig[8] = {0x89, 'H', 'D', 'F', '\r', '\n', 0x1a, '\n'};
+  FILE *f = fopen(path, "rb");
+  if (!f) return false;
+  bool yes = false;
+  for (long off : {0L, 512L, 1024L, 2048L}) {
+    unsigned char b[8];
+    if (fseek(f, off, SEEK_SET) != 0 || fread(b, 1, 8, f) != 8) break;
+    if (memcmp(b, sig, 8) == 0) { yes = true; break; }
+  }
+  fclose(f);
+  return yes;
+}
+
+constexpr int H5T_FLOAT_CLASS = 1, H5T_INTEGER_CLASS = 0;
+
+// One (time, lat, lon) field of a netCDF-4 file.  READ_PGF.f90:30 reads
+// variable 4; in a PGF file that is the only 3-D numeric variable (the
+// others are the time/lat/lon coordinates), which is what is looked for.
+struct H5Field {
+  const H5Api &a = h5();
+  hid_t_ file = -1, dset = -1, space = -1;
+  hsize_t_ dims[3] = {0, 0, 0};
+  ~H5Field() {
+    if (space >= 0) a.sclose(space);
+    if (dset >= 0) a.dclose(dset);
+    if (file >= 0) a.fclose(file);
+  }
+  bool open(const char *path) {
+    if (!a.ok || (file = a.fopen(path, 0u /* H5F_ACC_RDONLY */, 0)) < 0) return false;
+    char name[256];
+    for (hsize_t_ i = 0;; i++) {
+      if (a.lget_name_by_idx(file, ".", 0 /* H5_INDEX_NAME */, 0 /* H5_ITER_INC */, i, name, sizeof name, 0) < 0)
+        return false;
+      const hid_t_ d = a.dopen2(file, name, 0);
+      if (d < 0) continue;                          // a group, not a variable
+      const hid_t_ sp = a.dget_space(d), ty = a.dget_type(d);
+      const int cls = a.tget_class(ty);
+      a.tclose(ty);
+      if (a.sget_simple_extent_ndims(sp) == 3 && (cls == H5T_FLOAT_CLASS || cls == H5T_INTEGER_CLASS)) {
+        a.sget_simple_extent_dims(sp, dims, nullptr);
+        dset = d;
+        space = sp;
+        return true;
+      }
+      a.sclose(sp);
+      a.dclose(d);
+    }
+  }
+  // values of day t, (lat, lon) row-major, converted to float by HDF5
+  bool read_day(hsize_t_ t, float *out) {
+    const hsize_t_ start[3] = {t, 0, 0}, count[3] = {1, dims[1], dims[2]}, mdim[1] = {dims[1] * dims[2]};
+    if (a.sselect_hyperslab(space, 0 /* H5S_SELECT_SET */, start, nullptr, count, nullptr) < 0) return false;
+    const hid_t_ mem = a.screate_simple(1, mdim, nullptr);
+    const int rc = a.dread(dset, *a.native_float, mem, space, 0, out);
+    a.sclose(mem);
+    return rc >= 0;
+  }
+};
+
+// NTIMES of a netCDF-4 file: the 'time' dimension (its coordinate
+// variable), else the first dimension of the field
+long h5_ntimes(const char *path) {
+  const H5Api &a = h5();
+  if (!a.ok) return -1;
+  const hid_t_ f = a.fopen(path, 0u, 0);
+  if (f < 0) return -1;
+  long n = -1;
+  if (a.lexists(f, "time", 0) > 0) {
+    const hid_t_ d = a.dopen2(f, "time", 0);
+    if (d >= 0) {
+      const hid_t_ sp = a.dget_space(d);
+      hsize_t_ dd[4];
+      if (a.sget_simple_extent_ndims(sp) == 1 && a.sget_simple_extent_dims(sp, dd, nullptr) == 1) n = (long)dd[0];
+      a.sclose(sp);
+      a.dclose(d);
+    }
+  }
+  a.fclose(f);
+  if (n < 0) {
+    H5Field fld;
+    if (fld.open(path)) n = (long)fld.dims[0];
+  }
+  return n;
+}
 
 // ------------------------------------------------------------------ writer
 struct Att {
@@ -386,6 +548,21 @@ int h9g_nc_forcing_read(const char *const *paths, int nx, int ny, int ncell, con
   for (int k = 0; k < H9G_NFORCING; k++) {
     rc[k] = 0;
     th.emplace_back([&, k]() {
+      if (paths[k] && is_hdf5(paths[k])) {          // netCDF-4
+        H5Field fld;
+        if (!fld.open(paths[k]) || fld.dims[1] != (hsize_t_)ny || fld.dims[2] != (hsize_t_)nx ||
+            (hsize_t_)(t0 + nt) > fld.dims[0]) {
+          rc[k] = H9G_EINVAL;
+          return;
+        }
+        std::vector<float> slice((size_t)nx * ny);
+        for (int t = 0; t < nt; t++) {
+          if (!fld.read_day((hsize_t_)(t0 + t), slice.data())) { rc[k] = H9G_EINVAL; return; }
+          float *o = out + ((size_t)k * nt + t) * ncell;
+          for (int c = 0; c < ncell; c++) o[c] = slice[(size_t)gid[c]];
+        }
+        return;
+      }
       NcReader r;
       if (!paths[k] || !r.open(paths[k]) || r.vars.empty()) { rc[k] = H9G_EINVAL; return; }
       // varid = 4 (READ_PGF.f90:30) when it is the (time, lat, lon) float
@@ -418,6 +595,10 @@ int h9g_nc_forcing_read(const char *const *paths, int nx, int ny, int ncell, con
 
 // NTIMES of a PGF file (READ_NET_CDF_0D.f90: the 'time' dimension).
 int h9g_nc_ntimes(const char *path) {
+  if (path && is_hdf5(path)) {
+    const long n = h5_ntimes(path);
+    return n < 0 ? H9G_EINVAL : (int)n;
+  }
   NcReader r;
   if (!path || !r.open(path)) return H9G_EINVAL;
   const int d = r.dim_index("time");

@@ -151,6 +151,12 @@ INTERFACE
     REAL(C_DOUBLE), INTENT(OUT) :: host_out (*)
     INTEGER(C_INT) :: h9g_get_diagnostics
   END FUNCTION
+  FUNCTION h9g_get_errors (ctx, rec) BIND(C, NAME='h9g_get_errors')
+    IMPORT :: C_PTR, C_INT, C_INT32_T
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT32_T), INTENT(OUT) :: rec (*)
+    INTEGER(C_INT) :: h9g_get_errors
+  END FUNCTION
   FUNCTION h9g_get_diagnostics_async (ctx, dev_out, stream) &
            BIND(C, NAME='h9g_get_diagnostics_async')
     IMPORT :: C_PTR, C_INT

@@ -130,6 +130,11 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear);
 /* Wait for all work; returns the first STOP code raised, if any. */
 int h9g_sync(h9g_ctx *ctx);
 int h9g_last_error(h9g_ctx *ctx, h9g_error *err);
+/* Every cell's STOP record since the state was last set: rec is 4 rows of
+ * ncell int32 -- H9G_ERR_* code (0: none), 0-based day, substep, and the
+ * bits of the float value the reference prints (failed cells stop; their
+ * annual means are NaN). */
+int h9g_get_errors(h9g_ctx *ctx, int32_t *rec);
 
 /* --- LCLIM single-site path (HYBRID9.f90:339-480) ---------------------- */
 /* Runs nday days of the site path for every cell of the context: per
@@ -178,7 +183,9 @@ int h9g_synth_params(h9g_ctx *ctx, uint64_t seed);
 int h9g_synth_forcing(h9g_ctx *ctx, int slot, uint64_t seed, int day0,
                       int nday);
 
-/* --- NetCDF I/O (hybrid9_amd/csrc/h9g_io.cpp; classic CDF-1/2 files) --- */
+/* --- NetCDF I/O (hybrid9_amd/csrc/h9g_io.cpp): reads netCDF-4 (HDF5,
+ * through the image's libhdf5, loaded on first use) and classic CDF-1/2;
+ * writes CDF-2 ------------------------------------------------------------ */
 /* WRITE_NET_CDF_3DR.f90:93-263: annual means (h9g_get_annual layout, 12+L
  * rows of ncell) of the cells gid (grid ids iy*nx+ix, row iy from the
  * north) to axyYYYY.nc with the reference's dimensions, variable names,

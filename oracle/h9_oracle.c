@@ -652,7 +652,7 @@ static int days_in_year(int y) {   /* INIT.f90:844-859 (Gregorian) */
 int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
             const float *zi, const float *params, const float *forcing,
             float *state, float *annual, int ntrace, const int *trace_cells,
-            float *trace, int nthreads, h9o_error *err) {
+            float *trace, int nthreads, h9o_error *err, int *cell_err) {
   if (ncell < 0 || L < 3 || L > LM || nisurf < 1 || nyears < 1) return H9O_ERR_ARGS;
   int ndays = 0;
   for (int y = 0; y < nyears; y++) ndays += days_in_year(year0 + y);
@@ -680,7 +680,7 @@ int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
     float npp = zero;
     int day = 0, code = 0;
     float errval = 0.0f;
-    int eday = -1, estep = -1;
+    int eday = -1, estep = -1, edoy = -1;
     for (int y = 0; y < nyears && !code; y++) {
       const int nt = days_in_year(year0 + y);
       float npp_sum = zero, plant_mass_sum = zero, rnf_sum = zero, evap_sum = zero;
@@ -708,7 +708,7 @@ int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
         for (int ns = 0; ns < nisurf; ns++) {       /* :193-211 */
           float tran, evg;
           code = hydrology(&g, &p, &d, &s, &rnf_sum, theta, &tran, &evg, &errval);
-          if (code) { eday = day; estep = ns; break; }
+          if (code) { eday = day; estep = ns; edoy = dd; break; }
           if (trow) {
             float *r = trow + ((size_t)day * nisurf + ns) * tw;
             for (int i = 0; i < L; i++) {
@@ -758,6 +758,13 @@ int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
       a[(11 + L) * ncell + c] = h2osoi_sum_total / (float)nt;
     }
     store_st(&s, state, ncell, L, c);
+    if (cell_err) {   /* every cell's STOP record: code, day of year, substep, value bits */
+      cell_err[c] = code;
+      cell_err[(size_t)ncell + c] = code ? edoy : 0;
+      cell_err[2 * (size_t)ncell + c] = code ? estep : 0;
+      memcpy(&cell_err[3 * (size_t)ncell + c], &errval, 4);
+      if (!code) cell_err[3 * (size_t)ncell + c] = 0;
+    }
     if (code) {
 #pragma omp critical(h9o_err)
       {

@@ -61,7 +61,9 @@ int h9o_init_state(int ncell, int L, const float *zi, const float *params,
 int h9o_run(int ncell, int L, int nisurf, int grow_on, int year0, int nyears,
             const float *zi, const float *params, const float *forcing,
             float *state, float *annual, int ntrace, const int *trace_cells,
-            float *trace, int nthreads, h9o_error *err);
+            float *trace, int nthreads, h9o_error *err,
+            int *cell_err /* NULL, or 4 rows x ncell: STOP code, day of
+                             year, substep, value bits (h9g_get_errors) */);
 
 /* LCLIM single-site path (HYBRID9.f90:339-480), layouts of h9g_run_site:
  * sub (nday*nisurf, 5, ncell), daily (nday, 2, ncell), lai (nday, 3, ncell),

@@ -39,7 +39,7 @@ def lib():
         _lib.h9o_init_state.argtypes = [C.c_int, C.c_int, f, f, f]
         _lib.h9o_run.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  f, f, f, f, f, C.c_int, C.POINTER(C.c_int), f,
-                                 C.c_int, C.POINTER(H9OError)]
+                                 C.c_int, C.POINTER(H9OError), C.POINTER(C.c_int)]
         _lib.h9o_site.argtypes = [C.c_int] * 4 + [f] * 7 + [C.c_int, C.POINTER(H9OError)]
         i64 = C.POINTER(C.c_int64)
         _lib.h9o_soil_layer.argtypes = [C.c_int, C.c_int, C.c_int, i64, f, f, f, f, f, f, f, f]
@@ -87,12 +87,14 @@ def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=1,
     tc = np.asarray(sorted(trace_cells), dtype=np.int32)
     tr = np.zeros((max(len(tc), 1), ndays * nisurf, refcase.trace_width(L)), dtype=np.float32)
     err = H9OError()
+    rec = np.zeros((4, n), dtype=np.int32)
     rc = lib().h9o_run(n, L, nisurf, int(grow_on), year0, nyears, _fp(zi), _fp(pp), _fp(fo),
                        _fp(st), _fp(ann), len(tc), tc.ctypes.data_as(C.POINTER(C.c_int)),
-                       _fp(tr), nthreads, C.byref(err))
+                       _fp(tr), nthreads, C.byref(err), rec.ctypes.data_as(C.POINTER(C.c_int)))
     out = dict(annual=ann, state=refcase.unpack_state(st, n, L), rc=rc,
                err=dict(code=err.code, cell=err.cell, day=err.day, substep=err.substep,
-                        value=err.value))
+                        value=err.value),
+               errors=dict(code=rec[0], day=rec[1], substep=rec[2], value=rec[3].view(np.float32)))
     if len(tc):
         out["trace"] = tr
     return out

@@ -43,6 +43,18 @@ def load_golden(name):
         p, f = synth_inputs(gid, meta["year0"], meta["nyears"], L, meta["seed"])
         assert digest(packed_params(p), f) == meta["input_sha256"], "synthetic inputs drifted"
         state0 = None
+    elif meta["kind"] == "spinup":
+        from tests.golden.make_golden import spinup_inputs
+        gid = np.asarray(meta["gid"], dtype=np.int64)
+        ns = meta["n_synth"]
+        _, p, f, state0 = spinup_inputs(gid[:ns], gid[ns:], meta["year0"], meta["nyears"], L, meta["seed"])
+        assert digest(packed_params(p), f, state0) == meta["input_sha256"], "spin-up inputs drifted"
+    elif meta["kind"] == "l10":
+        from tests.golden.make_golden import l10_inputs
+        gid = np.asarray(meta["gid"], dtype=np.int64)
+        p, f = l10_inputs(gid, meta["year0"], meta["nyears"], meta["seed"])
+        assert digest(packed_params(p), f) == meta["input_sha256"], "L=10 inputs drifted"
+        state0 = None
     else:
         pp = z["params"]
         p = {k: pp[i * n * L:(i + 1) * n * L].reshape(n, L)
@@ -53,7 +65,7 @@ def load_golden(name):
     inputs = dict(zi=np.asarray(meta["zi"], np.float32), params=p, forcing=f,
                   nisurf=meta["nisurf"], year0=meta["year0"], nyears=meta["nyears"],
                   grow_on=meta["grow_on"], state0=state0)
-    expected = {k: z[k] for k in ("annual", "state", "trace") if k in z.files}
+    expected = {k: z[k] for k in ("annual", "state", "trace", "state_decade", "state_ok", "ok") if k in z.files}
     return meta, inputs, expected
 
 

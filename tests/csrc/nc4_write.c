@@ -1,0 +1,59 @@
+/* TEST HELPER: writes a netCDF-4 file the way libnetcdf lays one out in
+ * HDF5 -- coordinate variables time(time), lat(lat), lon(lon) made HDF5
+ * dimension scales, and one chunked, deflated float field
+ * <name>(time, lat, lon) with those scales attached -- so the HDF5 read
+ * path of h9g_io.cpp is tested on the on-disk form of a PGF v2.1 file
+ * (READ_NET_CDF_3DR.f90:95-97 reads it with nf90_get_var).
+ *   nc4_write <path> <name> <nt> <ny> <nx> <raw float32 file (nt*ny*nx)>
+ * Built by tests/test_netcdf.py: gcc ... -lhdf5_hl -lhdf5 (/opt/conda). */
+#include <hdf5.h>
+#include <hdf5_hl.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+static hid_t coord(hid_t f, const char *name, hsize_t n, const float *v) {
+  hid_t sp = H5Screate_simple(1, &n, NULL);
+  hid_t d = H5Dcreate2(f, name, H5T_IEEE_F32LE, sp, H5P_DEFAULT, H5P_DEFAULT, H5P_DEFAULT);
+  H5Dwrite(d, H5T_NATIVE_FLOAT, H5S_ALL, H5S_ALL, H5P_DEFAULT, v);
+  H5DSset_scale(d, name);
+  H5Sclose(sp);
+  return d;
+}
+
+int main(int argc, char **argv) {
+  if (argc != 7) return 2;
+  const hsize_t nt = atoi(argv[3]), ny = atoi(argv[4]), nx = atoi(argv[5]);
+  float *data = malloc(sizeof(float) * nt * ny * nx);
+  FILE *in = fopen(argv[6], "rb");
+  if (!in || fread(data, sizeof(float), nt * ny * nx, in) != nt * ny * nx) return 3;
+  fclose(in);
+  hid_t fapl = H5Pcreate(H5P_FILE_ACCESS);
+  H5Pset_libver_bounds(fapl, H5F_LIBVER_EARLIEST, H5F_LIBVER_LATEST);
+  hid_t fcpl = H5Pcreate(H5P_FILE_CREATE);
+  H5Pset_link_creation_order(fcpl, H5P_CRT_ORDER_TRACKED | H5P_CRT_ORDER_INDEXED);
+  hid_t f = H5Fcreate(argv[1], H5F_ACC_TRUNC, fcpl, fapl);
+  float *tv = malloc(sizeof(float) * nt), *yv = malloc(sizeof(float) * ny), *xv = malloc(sizeof(float) * nx);
+  for (hsize_t i = 0; i < nt; i++) tv[i] = (float)i;
+  for (hsize_t i = 0; i < ny; i++) yv[i] = 90.0f - (i + 0.5f) * 180.0f / ny;
+  for (hsize_t i = 0; i < nx; i++) xv[i] = -180.0f + (i + 0.5f) * 360.0f / nx;
+  hid_t dt = coord(f, "time", nt, tv), dy = coord(f, "lat", ny, yv), dx = coord(f, "lon", nx, xv);
+  hsize_t dims[3] = {nt, ny, nx}, chunk[3] = {1, ny, nx};
+  hid_t sp = H5Screate_simple(3, dims, NULL);
+  hid_t dcpl = H5Pcreate(H5P_DATASET_CREATE);
+  H5Pset_chunk(dcpl, 3, chunk);
+  H5Pset_shuffle(dcpl);
+  H5Pset_deflate(dcpl, 4);
+  hid_t dv = H5Dcreate2(f, argv[2], H5T_IEEE_F32LE, sp, H5P_DEFAULT, dcpl, H5P_DEFAULT);
+  H5Dwrite(dv, H5T_NATIVE_FLOAT, H5S_ALL, H5S_ALL, H5P_DEFAULT, data);
+  H5DSattach_scale(dv, dt, 0);
+  H5DSattach_scale(dv, dy, 1);
+  H5DSattach_scale(dv, dx, 2);
+  H5Dclose(dv);
+  H5Dclose(dt);
+  H5Dclose(dy);
+  H5Dclose(dx);
+  H5Sclose(sp);
+  H5Pclose(dcpl);
+  H5Fclose(f);
+  return 0;
+}

@@ -176,6 +176,127 @@ def edge_case():
     save("edge", meta, out, extra=dict(params=packed_params(p), forcing=f, state0=state0))
 
 
+# Config 4 spin-up cells with hand-set initial states / parameters /
+# rainfall (state field overrides, pr multiplier), applied to synthetic inputs
+SPINUP_EDGES = [
+    ("water table at the surface, wet column", dict(zwt=0.02, wet=0.95), 1.0),
+    ("water table in layer 3", dict(zwt=0.12), 1.0),
+    ("water table in layer 8", dict(zwt=1.5), 1.0),
+    ("saturated column", dict(zwt=0.5, wet=1.0), 1.0),
+    ("very dry, no rain", dict(wet=0.03), 0.0),
+    ("heavy rain x20: rising water table", dict(), 20.0),
+    ("aquifer near its 5000 mm cap, rain x10", dict(wa=4995.0, zwt=2.5), 10.0),
+    ("tight topsoil, rain x15 (qinmax)", dict(tight=1), 15.0),
+]
+
+
+def spinup_inputs(gid_syn, gid_edge, year0, nyears, L=8, seed=synth.SEED):
+    """Inputs of the config-4 spin-up golden: synthetic cells gid_syn from
+    the initial state of INIT.f90:707-811, then the SPINUP_EDGES cells."""
+    from oracle import port
+    gid = np.concatenate([gid_syn, gid_edge]).astype(np.int64)
+    p, f = synth_inputs(gid, year0, nyears, L, seed)
+    n0 = gid_syn.size
+    dz = np.diff(synth.ZI_L8)[:L]
+    for k, (_, ov, prs) in enumerate(SPINUP_EDGES):
+        if ov.get("tight"):
+            p["hksat"][n0 + k, :3] = np.float32(1.0e-5)
+        f[5, :, n0 + k] *= np.float32(prs)
+    st = refcase.unpack_state(port.init_state(p, synth.ZI_L8), gid.size, L)
+    for k, (_, ov, _) in enumerate(SPINUP_EDGES):
+        c = n0 + k
+        if "zwt" in ov:
+            st["zwt"][c] = np.float32(ov["zwt"])
+        if "wa" in ov:
+            st["wa"][c] = np.float32(ov["wa"])
+        if "wet" in ov:
+            st["h2osoi_liq"][c] = (np.float32(ov["wet"]) * p["theta_s"][c] * dz).astype(np.float32)
+    return gid, p, f, refcase.pack_state(st, L)
+
+
+def spinup_case(name="c4_spinup", year0=1901, nyears=20, decade=10):
+    """Config 4 (30-year spin-up) restated small: 24 cells, NS = 48, GROW on,
+    run as two decades with the state carried across, as HYBRID9.f90:93-130
+    carries it across its decade loop.  The reference is run over all years
+    at once and decade by decade; both must agree bit for bit (the packed
+    state is the whole per-cell state).  Stores the annual means of every
+    year, the state at the decade boundary and at the end."""
+    land = synth.land_cells()
+    gsyn, gedge = land[::4211][:16], land[2000::8000][:len(SPINUP_EDGES)]
+    gid, p, f, st0 = spinup_inputs(gsyn, gedge, year0, nyears)
+    kw = dict(zi=synth.ZI_L8, params=p, nisurf=48, grow_on=1)
+    whole = refcase.run_case(forcing=f, year0=year0, nyears=nyears, state0=refcase.unpack_state(st0, gid.size, 8),
+                             **kw)
+    nd1 = sum(synth.days_in_year(year0 + k) for k in range(decade))
+    d1 = refcase.run_case(forcing=f[:, :nd1], year0=year0, nyears=decade,
+                          state0=refcase.unpack_state(st0, gid.size, 8), **kw)
+    d2 = refcase.run_case(forcing=f[:, nd1:], year0=year0 + decade, nyears=nyears - decade,
+                          state0=d1["state"], **kw)
+    assert np.array_equal(np.concatenate([d1["annual"], d2["annual"]]), whole["annual"], equal_nan=True)
+    assert np.array_equal(refcase.pack_state(d2["state"], 8), refcase.pack_state(whole["state"], 8))
+    meta = dict(name=name, kind="spinup", seed=synth.SEED, gid=gid.tolist(), n_synth=int(gsyn.size),
+                edges=[e[0] for e in SPINUP_EDGES], L=8, ncell=int(gid.size), year0=year0, nyears=nyears,
+                decade=decade, nisurf=48, grow_on=1, zi=synth.ZI_L8.tolist(),
+                input_sha256=digest(packed_params(p), f, st0),
+                generator="oracle/_ref/h9ref (reference HYDROLOGY.f90/GROW.f90, amdflang -O2), "
+                          "whole run == decade-by-decade run")
+    np.savez_compressed(OUT / f"{name}.npz", meta=np.array(json.dumps(meta)), annual=whole["annual"],
+                        state=refcase.pack_state(whole["state"], 8),
+                        state_decade=refcase.pack_state(d1["state"], 8))
+    print(f"{name}: {gid.size} cells x {nyears} yr, {(OUT / f'{name}.npz').stat().st_size / 1e3:.0f} kB")
+
+
+def l10_inputs(gid, year0, nyears, seed=synth.SEED):
+    """Config 5 synthetic inputs: 0.25 deg cells, 10 soil layers."""
+    lat = synth.cell_lat(gid, synth.NX025, synth.NY025)
+    p = synth.make_params(gid, 10, seed)
+    nd = sum(synth.days_in_year(year0 + k) for k in range(nyears))
+    return p, synth.make_forcing(gid, lat, synth.year_day0(year0), nd, seed)
+
+
+def l10_case(name="c5_l10_sample", year0=1901, nyears=2, nisurf=24):
+    """Config 5 (0.25 deg, L = 10, NS = 24, GROW on) pinned to the reference:
+    oracle/_ref/h9ref_l10 is the unmodified HYDROLOGY.f90/GROW.f90 built
+    with nsoil_layers_max = 10, Nlevgrnd = 11 (make -C oracle ref10).
+    Cells: a sample of the 0.25 deg land grid plus land cell 773, whose
+    soil column reaches the water-imbalance STOP (HYDROLOGY.f90:1244) in
+    1901 (found by running the C oracle over all 270,000 cells).  The
+    reference STOPs the whole program there, so the STOP cell runs alone:
+    the fixture holds its STOP record and NaN means, the others' outputs."""
+    land = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)
+    stop_idx = [773]
+    sample = [i for i in range(977, land.size, 5413)][:48]
+    idx = sample + stop_idx
+    gid = land[idx].astype(np.int64)
+    p, f = l10_inputs(gid, year0, nyears)
+    ok = np.array([i not in stop_idx for i in idx])
+    sub = lambda a: {k: v[ok] for k, v in a.items()}  # noqa: E731
+    out = refcase.run_case(zi=synth.ZI_L10, params=sub(p), forcing=np.ascontiguousarray(f[:, :, ok]),
+                           nisurf=nisurf, year0=year0, nyears=nyears, grow_on=1)
+    n, L = gid.size, 10
+    annual = np.full((nyears, 12 + L, n), np.nan, np.float32)
+    annual[:, :, ok] = out["annual"]
+    stops = []
+    for c in np.where(~ok)[0]:
+        one = {k: v[c:c + 1] for k, v in p.items()}
+        try:
+            refcase.run_case(zi=synth.ZI_L10, params=one, forcing=np.ascontiguousarray(f[:, :, c:c + 1]),
+                             nisurf=nisurf, year0=year0, nyears=nyears, grow_on=1)
+        except refcase.RefStop as e:
+            stops.append(dict(cell=int(c), **{k: e.info[k] for k in ("code", "day", "value")}))
+        else:
+            raise SystemExit(f"{name}: cell {c} was expected to STOP")
+    meta = dict(name=name, kind="l10", seed=synth.SEED, gid=gid.tolist(), L=L, ncell=int(n), year0=year0,
+                nyears=nyears, nisurf=nisurf, grow_on=1, zi=synth.ZI_L10.tolist(), stops=stops,
+                input_sha256=digest(packed_params(p), f),
+                generator="oracle/_ref/h9ref_l10 (reference HYDROLOGY.f90/GROW.f90 with "
+                          "nsoil_layers_max=10, Nlevgrnd=11; amdflang -O2)")
+    st = refcase.pack_state(out["state"], L)
+    np.savez_compressed(OUT / f"{name}.npz", meta=np.array(json.dumps(meta)), annual=annual,
+                        state_ok=st, ok=ok)
+    print(f"{name}: {n} cells x {nyears} yr, STOPs {stops}, {(OUT / f'{name}.npz').stat().st_size / 1e3:.0f} kB")
+
+
 def site_inputs(gid, L, nisurf, years, events, seed=synth.SEED, soils="synth", ppt_scale=1.0):
     """Synthetic LCLIM site inputs (hybrid9_amd.site): soils of the land
     cells gid (soils="independent": independent_layer_params), site forcing
@@ -257,7 +378,12 @@ def main():
     stop_case("stop_ns24", land[263::527][90:98], nisurf=24)
     edge_case()
     main_lclim()
+    spinup_case()
+    l10_case()
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:
+        globals()[sys.argv[1]]()
+    else:
+        main()

@@ -79,3 +79,28 @@ def math_inputs(n=1 << 22, seed=7):
                    3e38, -3.0, 0.33333334, 2.8, 126.0, -150.0, 149.5], np.float32)
     gx, gy = np.meshgrid(sv, sv)
     return np.concatenate([xs, gx.ravel()]), np.concatenate([ys, gy.ravel()])
+
+
+CONDA = Path("/opt/conda")
+
+
+def nc4_writer_bin() -> Path | None:
+    """tests/csrc/nc4_write.c against the image's HDF5 (None if absent)."""
+    if not (CONDA / "include" / "hdf5.h").exists():
+        return None
+    src = ROOT / "tests" / "csrc" / "nc4_write.c"
+    out = BUILD / "nc4_write"
+    return _build(src, out, ["gcc", "-O1", f"-I{CONDA}/include", str(src), "-o", str(out),
+                             f"-L{CONDA}/lib", f"-Wl,-rpath,{CONDA}/lib", "-lhdf5_hl", "-lhdf5"])
+
+
+def write_nc4(path: Path, var: str, data: np.ndarray) -> Path:
+    """A netCDF-4 (HDF5) file with <var>(time, lat, lon) and its coordinate
+    dimension scales (nc4_write.c)."""
+    exe = nc4_writer_bin()
+    raw = path.with_suffix(".raw")
+    np.ascontiguousarray(data, np.float32).tofile(raw)
+    nt, ny, nx = data.shape
+    subprocess.run([str(exe), str(path), var, str(nt), str(ny), str(nx), str(raw)], check=True)
+    raw.unlink()
+    return path

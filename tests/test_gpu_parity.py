@@ -23,7 +23,7 @@ def _gpu_run(inp, L):
 
 
 @pytest.mark.parametrize("kernel", ["pair", "solo", "mixed"])
-@pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit")))
+@pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit", "spinup")))
 def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
     """Both year kernels (two lanes per column = the default; one lane), and
     both in one run (cells [0, 37) on the solo kernel, the rest on pair)."""
@@ -49,6 +49,51 @@ def test_gpu_reproduces_reference_stop(name, kernel, monkeypatch):
     assert f"{e['value']:.9g}" == f"{s['value']:.9g}"
 
 
+def test_config4_spinup_decades_carry_state():
+    """Config 4 (30-year spin-up) restated on 24 cells: the reference's
+    decade loop (HYBRID9.f90:93-130) carries every cell's state from one
+    decade's forcing slab to the next.  Here each decade is its own context
+    and the state crosses through h9g_get_state / h9g_set_state; the annual
+    means of all 20 years and the state at the boundary and at the end are
+    the reference's, bit for bit."""
+    meta, inp, exp = load_golden("c4_spinup")
+    dec = meta["decade"]
+    nd1 = sum(h.days_in_year(meta["year0"] + k) for k in range(dec))
+    common = dict(zi=inp["zi"], params=inp["params"], nisurf=inp["nisurf"], grow_on=bool(inp["grow_on"]))
+    d1 = h.run(forcing=inp["forcing"][:, :nd1], year0=meta["year0"], nyears=dec, state0=inp["state0"], **common)
+    assert d1["rc"] == 0, d1["err"]
+    assert same_bits(d1["state"], exp["state_decade"])
+    d2 = h.run(forcing=inp["forcing"][:, nd1:], year0=meta["year0"] + dec, nyears=meta["nyears"] - dec,
+               state0=d1["state"], **common)
+    assert d2["rc"] == 0, d2["err"]
+    assert same_bits(np.concatenate([d1["annual"], d2["annual"]]), exp["annual"])
+    assert same_bits(d2["state"], exp["state"])
+
+
+@pytest.mark.parametrize("kernel", ["pair", "solo", "mixed"])
+def test_config5_l10_matches_reference_golden(kernel, monkeypatch):
+    """Config 5 (0.25 deg, L = 10, NS = 24, GROW) against the reference
+    rebuilt with nsoil_layers_max = 10: every annual mean (NaN for the cell
+    that STOPs), the failed-cell set and its STOP record, and the end state
+    of the other cells, bit for bit, over 2 years."""
+    monkeypatch.setenv("H9G_KERNEL", kernel)
+    monkeypatch.setenv("H9G_SPLIT", "17")
+    meta, inp, exp = load_golden("c5_l10_sample")
+    ok = exp["ok"]
+    out = h.run(zi=inp["zi"], params=inp["params"], forcing=inp["forcing"], nisurf=inp["nisurf"],
+                year0=inp["year0"], nyears=inp["nyears"], grow_on=True, stop_on_error=False)
+    assert same_bits(out["annual"], exp["annual"])
+    e = out["errors"]
+    assert np.array_equal(np.nonzero(e["code"])[0], [s["cell"] for s in meta["stops"]])
+    for s in meta["stops"]:
+        c = s["cell"]
+        assert (e["code"][c], e["day"][c]) == (s["code"], s["day"])
+        assert f"{e['value'][c]:.9g}" == f"{s['value']:.9g}"
+    st = refcase.unpack_state(out["state"], meta["ncell"], meta["L"])
+    st = {k: v[ok] for k, v in st.items()}
+    assert same_bits(refcase.pack_state(st, meta["L"]), exp["state_ok"])
+
+
 def test_reference_stop_raises():
     meta, inp, _ = load_golden("stop_ns24")
     n = meta["ncell"]
@@ -62,7 +107,7 @@ def test_reference_stop_raises():
 
 
 def _full_grid_gpu(gid, L, nisurf, grow_on, year0, nyears, seed=synth.SEED, nx=synth.NX05,
-                   ny=synth.NY05):
+                   ny=synth.NY05, raise_on_stop=True):
     """Whole grid on the GPU with inputs generated on the device."""
     lat = synth.cell_lat(gid, nx, ny)
     zi = synth.ZI_L8 if L == 8 else synth.ZI_L10
@@ -75,10 +120,12 @@ def _full_grid_gpu(gid, L, nisurf, grow_on, year0, nyears, seed=synth.SEED, nx=s
             nt = synth.days_in_year(year0 + y)
             ctx.synth_forcing(y % 2, seed, synth.year_day0(year0 + y), nt)
             ctx.run_year(y % 2, year0 + y)
-            ctx.sync()
+            ctx.sync(raise_on_stop=raise_on_stop)
             anns.append(ctx.get_annual())
         state = ctx.get_state()
         diag = ctx.get_diagnostics()
+        if not raise_on_stop:
+            return np.stack(anns), state, diag, ctx.get_errors()
     return np.stack(anns), state, diag
 
 
@@ -121,12 +168,25 @@ def test_config5_l10_quarter_degree_sample(kernel, monkeypatch):
     (pinned at L=8 by the goldens)."""
     monkeypatch.setenv("H9G_KERNEL", kernel)
     monkeypatch.setenv("H9G_SPLIT", "1001")
-    gid = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)[::97][:2048]
-    ann, st, _ = _full_grid_gpu(gid, 10, 24, True, 1901, 1, nx=synth.NX025, ny=synth.NY025)
-    ref = _oracle_sample(gid, np.arange(gid.size), 10, 24, 1, 1901, 1, synth.NX025, synth.NY025)
-    ok = np.isfinite(ref["annual"][0, 2])
-    assert ok.sum() > 0.9 * gid.size
-    assert same_bits(ann[:, :, ok], ref["annual"][:, :, ok])
+    land = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)
+    # a 2048-cell sample plus land cell 773, which reaches the reference's
+    # water-imbalance STOP in 1901 (tests/golden/c5_l10_sample.npz)
+    gid = np.sort(np.concatenate([land[::97][:2047], land[773:774]]))
+    ann, st, _, errs = _full_grid_gpu(gid, 10, 24, True, 1901, 2, nx=synth.NX025, ny=synth.NY025,
+                                      raise_on_stop=False)
+    ref = _oracle_sample(gid, np.arange(gid.size), 10, 24, 1, 1901, 2, synth.NX025, synth.NY025)
+    # every field, NaN for the failed cells, and the same failed-cell set,
+    # STOP codes, days, substeps and values
+    assert same_bits(ann, ref["annual"])
+    re = ref["errors"]
+    assert np.count_nonzero(re["code"]) >= 1
+    for k in ("code", "day", "substep"):
+        assert np.array_equal(errs[k], re[k]), k
+    assert same_bits(errs["value"], re["value"])
+    ok = re["code"] == 0
+    got = refcase.unpack_state(st, gid.size, 10)
+    for k, v in ref["state"].items():
+        assert same_bits(got[k][ok], v[ok]), k
 
 
 def test_shard_invariance_and_determinism():

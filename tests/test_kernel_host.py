@@ -54,7 +54,7 @@ def host_run(*, zi, params, forcing, nisurf, year0, nyears, grow_on, state0, con
 
 # const_geo: 1/0 = compile-time / runtime layer geometry
 @pytest.mark.parametrize("const_geo", [1, 0])
-@pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit")))
+@pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit", "spinup")))
 def test_kernel_body_matches_reference_golden(name, const_geo):
     meta, inp, exp = load_golden(name)
     out = host_run(const_geo=const_geo, **inp)

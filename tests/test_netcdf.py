@@ -10,6 +10,8 @@ independent netCDF-classic implementation:
   record ('time' unlimited) and fixed layouts, CDF-1 and CDF-2.
 The reference ships no netCDF files, so the fixtures are written here with
 scipy in the reference's layout."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 from scipy.io import netcdf_file
@@ -128,3 +130,32 @@ def test_forcing_reader_rejects_bad_inputs(tmp_path):
         h.nc_forcing_read(paths, NX + 1, NY, gid, 0, 2)      # wrong grid
     with pytest.raises(h.H9GError):
         h.nc_forcing_read(paths[:6] + [tmp_path / "missing.nc"], NX, NY, gid, 0, 2)
+
+
+@pytest.mark.skipif(not Path("/opt/conda/include/hdf5.h").exists(), reason="no HDF5 in this image")
+def test_forcing_reader_netcdf4_equals_cdf2(tmp_path):
+    """PGF v2.1 ships netCDF-4 (HDF5) files; READ_NET_CDF_3DR.f90:95-97 reads
+    days of <var>(time, lat, lon).  The same data written as netCDF-4 (HDF5
+    dimension-scale layout, chunked + deflate, tests/csrc/nc4_write.c) and
+    as CDF-2 read back identically, gathered at the same cells."""
+    from tests.helpers import write_nc4
+    rng = np.random.default_rng(4)
+    nt = 33
+    data = [rng.uniform(200, 300, (nt, NY, NX)).astype(np.float32) for _ in range(7)]
+    d4, d2 = tmp_path / "nc4", tmp_path / "cdf2"
+    d4.mkdir()
+    d2.mkdir()
+    p4 = [write_nc4(d4 / f"{v}_pgfv2.1_1901-1910.nc4", v, data[k]) for k, v in enumerate(h.PGF_VARS)]
+    p2 = [write_pgf_like(d2, v, data[k], 2) for k, v in enumerate(h.PGF_VARS)]
+    assert open(p4[0], "rb").read(4) == b"\x89HDF"
+    assert h.nc_ntimes(p4[0]) == nt
+    gid = rng.choice(NX * NY, 41, replace=False).astype(np.int64)
+    got4 = h.nc_forcing_read(p4, NX, NY, gid, 3, 25)
+    got2 = h.nc_forcing_read(p2, NX, NY, gid, 3, 25)
+    assert np.array_equal(got4, got2)
+    for k in range(7):
+        np.testing.assert_array_equal(got4[k], data[k].reshape(nt, -1)[3:28][:, gid])
+    with pytest.raises(h.H9GError):
+        h.nc_forcing_read(p4, NX, NY, gid, 20, 20)            # past NTIMES
+    with pytest.raises(h.H9GError):
+        h.nc_forcing_read(p4, NX, NY + 2, gid, 0, 2)          # wrong grid

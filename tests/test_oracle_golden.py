@@ -8,7 +8,7 @@ from oracle import port, refcase
 from tests.conftest import golden_names, load_golden, same_bits
 
 
-@pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit")))
+@pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit", "spinup")))
 def test_oracle_matches_reference_golden(name):
     meta, inp, exp = load_golden(name)
     L, n = meta["L"], meta["ncell"]
@@ -46,3 +46,20 @@ def test_oracle_is_cell_order_independent():
     out = port.run(zi=inp["zi"], params=p, forcing=inp["forcing"][:, :, sub], nisurf=48,
                    year0=1901, nyears=1, grow_on=1)
     assert same_bits(out["annual"], exp["annual"][:, :, sub])
+
+
+def test_oracle_matches_reference_l10_golden():
+    """Config 5 (L = 10) against the reference rebuilt with
+    nsoil_layers_max = 10 (oracle/_ref/h9ref_l10), including a cell that
+    reaches the water-imbalance STOP: NaN means for it, its STOP record,
+    and the other cells' annual means and end state bit for bit."""
+    meta, inp, exp = load_golden("c5_l10_sample")
+    L, ok = meta["L"], exp["ok"]
+    out = port.run(zi=inp["zi"], params=inp["params"], forcing=inp["forcing"], nisurf=inp["nisurf"],
+                   year0=inp["year0"], nyears=inp["nyears"], grow_on=inp["grow_on"], nthreads=4)
+    assert same_bits(out["annual"], exp["annual"])
+    (s,) = meta["stops"]
+    assert out["rc"] == s["code"] and out["err"]["cell"] == s["cell"] and out["err"]["day"] == s["day"]
+    assert f"{out['err']['value']:.9g}" == f"{s['value']:.9g}"
+    st = {k: (v[ok] if v.ndim else v) for k, v in out["state"].items()}
+    assert same_bits(refcase.pack_state(st, L), exp["state_ok"])
