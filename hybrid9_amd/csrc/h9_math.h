@@ -246,8 +246,11 @@ H9_HD float powf_nx(float x, float y, const Tabs &T, bool &special) {
   const double logx = log2_inline(ix, T);
   const double ylogx = (double)y * logx;
   // (| on bools: evaluate every test, no branches)
+  // |y log2 x| >= 126 on the high word: ((bits >> 47) & 0xffff) >= 0x80bf
+  // <=> (hi & 0x7fff8000) >= 0x405f8000 (a 32-bit compare, not 64-bit)
+  const uint32_t hi = (uint32_t)(asu64(ylogx) >> 32);
   special |= (int)(ix - 0x00800000u >= 0x7f800000u - 0x00800000u) | (int)(CheckY && zeroinfnan(iy)) |
-             (int)(((asu64(ylogx) >> 47) & 0xffff) >= (asu64(126.0) >> 47));
+             (int)((hi & 0x7fff8000u) >= 0x405f8000u);
   return exp2_inline(ylogx, 0, T);
 }
 

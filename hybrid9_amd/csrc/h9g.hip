@@ -105,7 +105,7 @@ h9g_pair_kernel(const KArgs a, const G g) {
   __shared__ uint64_t s_e2[32];
   __shared__ double s_l2[32];
   __shared__ float s_cell[H9G_PWAVES][PS::ROWS * H9G_PLANES];   // [wave][row][lane]
-  __shared__ float s_zt[2 * (L + 2)];
+  __shared__ float s_zt[zt_size<L>()];
   if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};
@@ -159,14 +159,14 @@ h9g_pair_kernel(const KArgs a, const G g) {
   float errval = 0.0f;
 #if defined(H9G_STAMPS)
   StampProf pr{stamp_clock(), {0, 0, 0, 0, 0, 0, 0, 0}};
-  const int code = cell_year_pair<L, G, Split2, PS, true>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar, a.nt,
-                                                         a.nisurf, a.grow_on, a.annual + c, (size_t)n, eday,
+  const int code = cell_year_pair<L, G, Split2, PS, true>(g, cs, sp, s, (const gbl_float *)(a.forc + c), (size_t)n, a.fvar, a.nt,
+                                                         a.nisurf, a.grow_on, (gbl_float *)(a.annual + c), (size_t)n, eday,
                                                          estep, errval, T, pr);
   if (lane == 0 && a.stamps)
     for (int k = 0; k < 8; k++) a.stamps[(blockIdx.x * H9G_PWAVES + wave) * 8 + k] = pr.acc[k];
 #else
-  const int code = cell_year_pair<L, G>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar, a.nt, a.nisurf,
-                                        a.grow_on, a.annual + c, (size_t)n, eday, estep, errval, T);
+  const int code = cell_year_pair<L, G>(g, cs, sp, s, (const gbl_float *)(a.forc + c), (size_t)n, a.fvar, a.nt, a.nisurf,
+                                        a.grow_on, (gbl_float *)(a.annual + c), (size_t)n, eday, estep, errval, T);
 #endif
   if (h != 0) return;                // the even lane writes the cell back
   int cw = c;
@@ -209,7 +209,7 @@ h9g_solo_kernel(const KArgs a, const G g) {
   __shared__ uint64_t s_e2[32];
   __shared__ double s_l2[32];
   __shared__ float s_cell[SS::ROWS * H9G_YBLOCK];
-  __shared__ float s_zt[2 * (L + 2)];
+  __shared__ float s_zt[zt_size<L>()];
   if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};
@@ -252,8 +252,8 @@ h9g_solo_kernel(const KArgs a, const G g) {
   cell_inv_pair<L, G>(g, cs);
   int eday = 0, estep = 0;
   float errval = 0.0f;
-  const int code = cell_year_pair<L, G, SplitAll, SS, false>(g, cs, sp, s, a.forc + c, (size_t)n, a.fvar,
-                                                             a.nt, a.nisurf, a.grow_on, a.annual + c,
+  const int code = cell_year_pair<L, G, SplitAll, SS, false>(g, cs, sp, s, (const gbl_float *)(a.forc + c), (size_t)n, a.fvar,
+                                                             a.nt, a.nisurf, a.grow_on, (gbl_float *)(a.annual + c),
                                                              (size_t)n, eday, estep, errval, T);
   int cw = c;
   opaque(cw);
@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(64) h9g_site_kernel(const SiteArgs a, const G 
   __shared__ uint64_t s_e2[32];
   __shared__ double s_l2[32];
   __shared__ float s_cell[SS::ROWS * 64];
-  __shared__ float s_zt[2 * (L + 2)];
+  __shared__ float s_zt[zt_size<L>()];
   if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};

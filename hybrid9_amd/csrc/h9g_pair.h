@@ -110,6 +110,7 @@ struct FlatStore {                     // host: one flat array per cell
   const float *zt;                     // zi(0..L+1), then zi(0..L+1)/1000
   H9K_HD float zi(int i) const { return zt[i]; }
   H9K_HD float zim(int i) const { return zt[L + 2 + i]; }
+  H9K_HD double rdz_t(int i) const { return join_d(zt[2 * (L + 2) + 2 * i], zt[2 * (L + 2) + 2 * i + 1]); }
   H9K_HD float lay(int p, int i) const { return b[p * L + i - 1]; }
   H9K_HD void set_lay(int p, int i, float v) const { b[p * L + i - 1] = v; }
   H9K_HD float sc(int k) const { return b[PF_N * L + k]; }
@@ -170,6 +171,9 @@ struct PairStore {
   float *svw;                          // this workgroup's rollback block (global)
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
+  __device__ __forceinline__ double rdz_t(int i) const {
+    return join_d(zt[2 * (L + 2) + 2 * i], zt[2 * (L + 2) + 2 * i + 1]);
+  }
   __device__ __forceinline__ float lay(int p, int i) const {
     return even[(p * NT + ((i - 1) >> 1)) * S + ((i - 1) & 1)];
   }
@@ -249,6 +253,9 @@ struct SoloStore {
   H9K_HD static constexpr int kr(int k) { return k < PS_LAI ? k : k - (PS_SVZWT - PS_LAI); }
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
+  __device__ __forceinline__ double rdz_t(int i) const {
+    return join_d(zt[2 * (L + 2) + 2 * i], zt[2 * (L + 2) + 2 * i + 1]);
+  }
   __device__ __forceinline__ float lay(int p, int i) const { return b[(pr(p) * L + i - 1) * 64]; }
   __device__ __forceinline__ void set_lay(int p, int i, float v) const { b[(pr(p) * L + i - 1) * 64] = v; }
   __device__ __forceinline__ float sc(int k) const { return b[(NPF * L + kr(k)) * 64]; }
@@ -428,14 +435,22 @@ H9K_HD void visit_layers(M &m, F visit) {
   }
 }
 
-// Runtime-indexable geometry table: zi(0..L+1), then zi(0..L+1)/1000
-// (the reference's zi(I)/1000.0, e.g. HYDROLOGY.f90:499-508,998).
+// Runtime-indexable geometry table (zt_size(L) floats): zi(0..L+1), then
+// zi(0..L+1)/1000 (the reference's zi(I)/1000.0, e.g. HYDROLOGY.f90:
+// 499-508,998), then RN64(1/dz(I)) for I = 0..L+1 as (low, high) words
+// (I = 0 unused).  A lane reads its own layers' values at a runtime index
+// instead of keeping compile-time selects live in registers.
+template <int L>
+constexpr int zt_size() { return 4 * (L + 2); }
 template <int L, class G, class T>
 H9K_HD void fill_zt(const G &g, T *zt) {
 #pragma unroll
   for (int i = 0; i <= L + 1; i++) {
     zt[i] = g.zi(i);
     zt[L + 2 + i] = g.zi(i) / 1000.0f;
+    const double r = (i > 0 && i <= L) ? g.rdz(i) : 0.0;
+    zt[2 * (L + 2) + 2 * i] = lo_d(r);
+    zt[2 * (L + 2) + 2 * i + 1] = hi_d(r);
   }
 }
 
@@ -592,9 +607,9 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     float *const out[1] = {zq};
     sp.template par<NT, 1>(
         [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
-          const int i0 = 2 * t + 1;                           // own layer i = i0 + h
-          const float zlo = sel(h, g.zi(i0 - 1), g.zi(i0));   // zi(i-1)
-          const float zhi = sel(h, g.zi(i0), g.zi(i0 + 1));   // zi(i)
+          const int i0 = 2 * t + 1;                           // own layer il = i0 + h
+          const int il = i0 + h;
+          const float zlo = cs.zi(il - 1), zhi = cs.zi(il);   // zi(i-1), zi(i): geometry table
           const float ts = OWN(PF_TS), psi = OWN(PF_PSI);
           float vol_eq;
           if (zwtmm <= zlo) {
@@ -608,8 +623,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
             if ((zwtmm < zhi) && (zwtmm > zlo)) {
               const float tempi = one;
               const float voleq1 = OWN(PF_PTE) / (zwtmm - zlo) * (tempi - temp0);
-              vol_eq = m.div(voleq1 * (zwtmm - zlo) + ts * (zhi - zwtmm), sel(h, g.dz(i0), g.dz(i0 + 1)),
-                             seld(h, g.rdz(i0), g.rdz(i0 + 1)));
+              vol_eq = m.div(voleq1 * (zwtmm - zlo) + ts * (zhi - zwtmm), zhi - zlo, cs.rdz_t(il));   // dz(i)
               vol_eq = MINF(ts, vol_eq);
               vol_eq = MAXF(vol_eq, zero);
             } else {
@@ -779,8 +793,22 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   for (int i = 1; i <= L; i++) h2o[i] = h2o[i] + dwat2[i] * g.dz(i);
   cs.launder();
   pr.mark(4);
-  // :856-904 recharge
-  float qcharge;
+  // The specific yield s_y(I) = max(ts(I) (1 - (1 + zwtmm/(-psi(I)))^(-1/b(I))),
+  // 0.02) (:963-965, :979-981, :1077-1080), for a layer i at runtime.
+  auto s_y_base = [&](int i, float zmm) __attribute__((always_inline)) -> float {
+    return one + divr<CS::kRecip>(m, zmm, -cs.lay(PF_PSI, i), [&]() { return lay_d(cs, PF_RPSI0, i); });
+  };
+  auto s_y_of = [&](int i, float pw) __attribute__((always_inline)) -> float {
+    return MAXF(cs.lay(PF_TS, i) * (one - pw), 0.02f);
+  };
+  auto s_y_at = [&](int i, float zmm) __attribute__((always_inline)) -> float {
+    return s_y_of(i, m.powf(s_y_base(i, zmm), cs.lay(PF_NINVB, i)));
+  };
+  // :856-904 recharge.  With the water table in the column, the power of
+  // the recharge conductivity ka (:874-877) and the power of the first
+  // layer the water-table loops below visit, s_y(jwt+1) at this zwtmm, are
+  // independent: one lane of the pair evaluates each.
+  float qcharge, sy_first = zero;
   if (jwt < L) {
     float th_j = zero, ts_j = one, hks_j = zero, bsw_j = zero, smp_m = zero, zq_m = zero, zc_j = zero;
 #pragma unroll
@@ -792,7 +820,15 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     const float wh_zwt = zero;
     const float s_node = MAXF(th_j / ts_j, 0.01f);
     const float s1 = MINF(one, s_node);
-    const float ka = hks_j * m.powf(s1, 2.0f * bsw_j + 3.0f);
+    FV<1> pK, pS;
+    sp.template pick<1>(
+        [&](int h) __attribute__((always_inline)) -> FV<1> {
+          const float b = h ? s_y_base(jwt + 1, zwtmm) : s1;
+          return FV<1>{{m.powf(b, sel(h, 2.0f * bsw_j + 3.0f, cs.lay(PF_NINVB, jwt + 1)))}};
+        },
+        pK, pS);
+    sy_first = s_y_of(jwt + 1, pS.v[0]);
+    const float ka = hks_j * pK.v[0];
     const float smp1m = MAXF(smpmin, smp_m);
     const float wh = smp1m - zq_m;
     if (jwt == 0)
@@ -804,14 +840,10 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   } else {
     qcharge = m.div(dwat2[L + 1] * dzA, dt, g.rdt());
   }
-  // :923-1009 water table from recharge.  The specific yield s_y(I)
-  // (:963-965, :979-981, :1077-1080) is evaluated for exactly the layers the
-  // loops visit (usually one), at a runtime layer index; rous = s_y(L) of
-  // the pre-update zwtmm came from the pair split above.
-  auto s_y_at = [&](int i, float zmm) __attribute__((always_inline)) -> float {
-    const float q = divr<CS::kRecip>(m, zmm, -cs.lay(PF_PSI, i), [&]() { return lay_d(cs, PF_RPSI0, i); });
-    return MAXF(cs.lay(PF_TS, i) * (one - m.powf((one + q), cs.lay(PF_NINVB, i))), 0.02f);
-  };
+  // :923-1009 water table from recharge.  s_y(I) is evaluated for exactly
+  // the layers the loops visit (usually one), at a runtime layer index (the
+  // first visit's from the pick above); rous = s_y(L) of the pre-update
+  // zwtmm came from the pair split of the equilibrium profile.
   float rous = MAXF(TS(L) * (one - pY.v[0]), 0.02f);
   int jwt2 = jwt;
   if (jwt == L) {
@@ -822,7 +854,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     if (qcharge_tot > zero) {          // rising: I = jwt+1 .. 1
       visit_layers(m, [&](int k) __attribute__((always_inline)) -> bool {
         const int i = jwt + 1 - k;
-        const float s_y = s_y_at(i, zwtmm);
+        const float s_y = k == 0 ? sy_first : s_y_at(i, zwtmm);
         float qcl = MINF(qcharge_tot, s_y * (zwtmm - cs.zi(i - 1)));
         qcl = MAXF(qcl, zero);
         if (s_y > zero) s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
@@ -832,7 +864,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     } else {                            // deepening: I = jwt+1 .. L
       visit_layers(m, [&](int k) __attribute__((always_inline)) -> bool {
         const int i = jwt + 1 + k;
-        const float s_y = s_y_at(i, zwtmm);
+        const float s_y = k == 0 ? sy_first : s_y_at(i, zwtmm);
         float qcl = MAXF(qcharge_tot, -s_y * (cs.zi(i) - zwtmm));
         qcl = MINF(qcl, zero);
         qcharge_tot = qcharge_tot - qcl;
@@ -849,13 +881,20 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   }
   cs.launder();
   pr.mark(5);
-  // :1015-1035 baseflow; s_y(L) for the new zwtmm (:1077-1080)
+  // :1015-1035 baseflow; s_y(L) for the new zwtmm (:1077-1080) on one lane
+  // of the pair, the drainage loop's first layer s_y(jwt2+1) on the other
   zwtmm = 1000.0f * s.zwt;
   float rsub_top = 5.5E-3f * m.expf(-fff * s.zwt);
-  rous = MAXF(TS(L) * (one - m.powf((one + divr<CS::kRecip>(m, zwtmm, -PSI(L),
-                                                                [&]() { return lay_d(cs, PF_RPSI0, L); })),
-                                    LAYF(PF_NINVB, L))),
-              0.02f);
+  const int jd = jwt2 < L ? jwt2 + 1 : L;
+  FV<1> pR, pD;
+  sp.template pick<1>(
+      [&](int h) __attribute__((always_inline)) -> FV<1> {
+        const int i = h ? jd : L;
+        return FV<1>{{m.powf(s_y_base(i, zwtmm), cs.lay(PF_NINVB, i))}};
+      },
+      pR, pD);
+  rous = s_y_of(L, pR.v[0]);
+  const float sy_drain = s_y_of(jd, pD.v[0]);
   // :1048-1118
   int jwt3 = jwt2;
   if (jwt2 == L) {
@@ -868,7 +907,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     if (rsub_top_tot > zero) { errval = rsub_top_tot; return 3; }
     visit_layers(m, [&](int k) __attribute__((always_inline)) -> bool {   // I = jwt+1 .. L
       const int i = jwt2 + 1 + k;
-      const float s_y = s_y_at(i, zwtmm);
+      const float s_y = k == 0 ? sy_drain : s_y_at(i, zwtmm);
       float rstl = MAXF(rsub_top_tot, -(s_y * (cs.zi(i) - zwtmm)));
       rstl = MINF(rstl, zero);
 #pragma unroll
@@ -1033,12 +1072,12 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
 // Park = keep the plant state in the store over the substeps (register
 // relief for the 168-VGPR pair kernel).
 template <int L, class G, class SP, class CS, bool Park = true, class PR = NoProf>
-H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float *forc, size_t fday,
-                          size_t fvar, int nt, int nisurf, int grow_on, float *acc, size_t astride,
+H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_float *forc, size_t fday,
+                          size_t fvar, int nt, int nisurf, int grow_on, gbl_float *acc, size_t astride,
                           int &eday, int &estep, float &errval, const h9m::Tabs &T, PR &&pr = PR()) {
   enum { A_NPP = 0, A_PM, A_RNF, A_EVAP, A_TAS, A_RLDS, A_RSDS, A_HUSS, A_PS, A_PR, A_RHS,
          A_THETA, A_H2O = 11 + L };
-  float *A = acc;
+  gbl_float *A = acc;
   const size_t as = astride;
   float rnf_sum = zero;
 #pragma unroll
@@ -1062,7 +1101,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float
   for (int day = 0; day < nt; day++) {
     cs.launder();
     opaque(A);
-    const float *f = forc + (size_t)day * fday;
+    const gbl_float *f = forc + (size_t)day * fday;
     opaque(f);
     {
       const Day d = make_day(f[0 * fvar], f[1 * fvar], f[2 * fvar], f[3 * fvar], f[4 * fvar],
@@ -1094,23 +1133,33 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const float
       grow_day<L, G, MathExact>(g, tas, s, cs, npp, me);              // :217
       park();
     }
-    A[A_TAS * as] = A[A_TAS * as] + tas;                              // :235-254
-    A[A_RLDS * as] = A[A_RLDS * as] + rlds;
-    A[A_RSDS * as] = A[A_RSDS * as] + rsds;
-    A[A_HUSS * as] = A[A_HUSS * as] + huss;
-    A[A_PS * as] = A[A_PS * as] + ps;
-    A[A_PR * as] = A[A_PR * as] + pr;
-    A[A_RHS * as] = A[A_RHS * as] + rhs;
-    A[A_PM * as] = A[A_PM * as] + s.pm;
-    A[A_NPP * as] = A[A_NPP * as] + npp;
-    float h2o_sum = A[A_H2O * as];
+    // :235-254.  All running sums are loaded before any is stored, so the
+    // loads issue back to back (the compiler cannot prove the strided
+    // fields distinct)
+    float a[12 + L];
+#pragma unroll
+    for (int k = 0; k < 12 + L; k++)
+      if (k != A_RNF && k != A_EVAP) a[k] = A[k * as];
+    a[A_TAS] = a[A_TAS] + tas;
+    a[A_RLDS] = a[A_RLDS] + rlds;
+    a[A_RSDS] = a[A_RSDS] + rsds;
+    a[A_HUSS] = a[A_HUSS] + huss;
+    a[A_PS] = a[A_PS] + ps;
+    a[A_PR] = a[A_PR] + pr;
+    a[A_RHS] = a[A_RHS] + rhs;
+    a[A_PM] = a[A_PM] + s.pm;
+    a[A_NPP] = a[A_NPP] + npp;
+    float h2o_sum = a[A_H2O];
 #pragma unroll
     for (int i = 1; i <= L; i++) {
       const float theta = MAXF(s.h2o[i], 1.0E-6f) / g.thk(i);       // HYDROLOGY.f90:1233
-      A[(A_THETA + i - 1) * as] = A[(A_THETA + i - 1) * as] + theta;
+      a[A_THETA + i - 1] = a[A_THETA + i - 1] + theta;
       h2o_sum = h2o_sum + s.h2o[i];
     }
-    A[A_H2O * as] = h2o_sum;
+    a[A_H2O] = h2o_sum;
+#pragma unroll
+    for (int k = 0; k < 12 + L; k++)
+      if (k != A_RNF && k != A_EVAP) A[k * as] = a[k];
   }
   // :263-290
   opaque(A);

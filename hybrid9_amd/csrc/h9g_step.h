@@ -173,8 +173,13 @@ enum : int { DR_N = 2 * DRP_N + DR_N1 };
 
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(3))) float lds_float;
+// Global-memory float: loads and stores through it cannot alias LDS, so
+// they are not ordered against the store's LDS traffic (a generic pointer
+// makes them flat_load/flat_store with a full wait after each).
+typedef __attribute__((address_space(1))) float gbl_float;
 #else
 typedef float lds_float;
+typedef float gbl_float;
 #endif
 
 template <int L>

@@ -26,7 +26,7 @@ static int run_cells_pair(const G &g, int n, int nisurf, int grow_on, int year0,
   int first = 0;
 #pragma omp parallel for schedule(dynamic, 4)
   for (int c = 0; c < n; c++) {
-    float store[FlatStore<L>::N], zt[2 * (L + 2)];
+    float store[FlatStore<L>::N], zt[zt_size<L>()];
     fill_zt<L>(g, zt);
     FlatStore<L> cs{store, zt};
     const SplitAll sp;
@@ -102,7 +102,7 @@ static int run_site_cells(const G &g, int n, int nday, int nisurf, const float *
   int first = 0;
 #pragma omp parallel for schedule(dynamic, 1)
   for (int c = 0; c < n; c++) {
-    float store[FlatStore<L>::N], zt[2 * (L + 2)];
+    float store[FlatStore<L>::N], zt[zt_size<L>()];
     fill_zt<L>(g, zt);
     FlatStore<L> cs{store, zt};
     St<L> s;
