@@ -115,6 +115,7 @@ def lib() -> C.CDLL:
         "h9g_kernel_name": (C.c_char_p, [vp]),
         "h9g_math_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP]),
         "h9g_div_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP, C.POINTER(C.c_int)]),
+        "h9g_math_fast_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP, C.POINTER(C.c_int)]),
         "h9g_synth_host": (C.c_int, [C.c_uint64, C.c_int, C.c_int, _I64P, _FP, C.c_int,
                                      C.c_int, _FP, _FP]),
         "h9g_land_cells": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint64, _I64P, _FP]),

@@ -649,7 +649,7 @@ __global__ void h9g_div_kernel(int n, const float *x, const float *d, float *out
   if (i >= n) return;
   MathFast mf{{nullptr, nullptr}, false};
   out[i] = mf.div(x[i], d[i], recip64(d[i]));
-  flag[i] = mf.special ? 1 : 0;
+  flag[i] = (mf.special || mf.redone) ? 1 : 0;     // 1: the quotient was redone as x / d
 }
 
 __global__ void h9g_math_kernel(int n, const float *x, const float *y, float *out) {
@@ -660,6 +660,19 @@ __global__ void h9g_math_kernel(int n, const float *x, const float *y, float *ou
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   out[i] = y ? h9m::powf(x[i], y[i], T) : h9m::expf(x[i], T);
+}
+
+// The year kernels' math (MathFast: glibc's main path, the rest redone in
+// place); flag = 1 where it was redone.
+__global__ void h9g_math_fast_kernel(int n, const float *x, const float *y, float *out, int *flag) {
+  __shared__ uint64_t s_e2[32];
+  __shared__ double s_l2[32];
+  load_tabs(s_e2, s_l2);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  MathFast mf{{s_e2, s_l2}, false};
+  out[i] = y ? mf.powf(x[i], y[i]) : mf.expf(x[i]);
+  flag[i] = mf.redone ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1242,6 +1255,15 @@ int h9g_sync(h9g_ctx *ctx) {
     unsigned long long cnt = 0;
     HIPCHK(hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(h9g_exact_count), sizeof(cnt)));
     fprintf(stderr, "h9g exact re-runs (lanes, cumulative): %llu\n", cnt);
+    std::vector<unsigned> w(1 << 16);
+    HIPCHK(hipMemcpyFromSymbol(w.data(), HIP_SYMBOL(h9g_exact_wave), sizeof(unsigned) << 16));
+    std::vector<std::pair<unsigned, int>> top;
+    for (int i = 0; i < (1 << 16); i++)
+      if (w[i]) top.push_back({w[i], i});
+    std::sort(top.rbegin(), top.rend());
+    fprintf(stderr, "h9g exact re-runs: %zu waves;", top.size());
+    for (size_t k = 0; k < top.size() && k < 8; k++) fprintf(stderr, " w%d:%u", top[k].second, top[k].first);
+    fprintf(stderr, "\n");
   }
 #endif
   int flag = 0;
@@ -1542,6 +1564,28 @@ int h9g_math_selftest(int device, int n, const float *x, const float *y, float *
   (void)hipFree(dx);
   (void)hipFree(dy);
   (void)hipFree(dout);
+  return 0;
+}
+
+int h9g_math_fast_selftest(int device, int n, const float *x, const float *y, float *out, int *flag) {
+  if (n <= 0 || !x || !out || !flag) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(device));
+  float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+  int *dflag = nullptr;
+  HIPCHK(hipMalloc(&dx, sizeof(float) * n));
+  HIPCHK(hipMalloc(&dout, sizeof(float) * n));
+  HIPCHK(hipMalloc(&dflag, sizeof(int) * n));
+  if (y) HIPCHK(hipMalloc(&dy, sizeof(float) * n));
+  HIPCHK(hipMemcpy(dx, x, sizeof(float) * n, hipMemcpyHostToDevice));
+  if (y) HIPCHK(hipMemcpy(dy, y, sizeof(float) * n, hipMemcpyHostToDevice));
+  h9g_math_fast_kernel<<<(n + 255) / 256, 256>>>(n, dx, dy, dout, dflag);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, sizeof(float) * n, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(flag, dflag, sizeof(int) * n, hipMemcpyDeviceToHost));
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  (void)hipFree(dout);
+  (void)hipFree(dflag);
   return 0;
 }
 

@@ -35,6 +35,7 @@
 
 #if defined(H9G_COUNT_EXACT)
 __device__ unsigned long long h9g_exact_count;   // exact re-runs (lanes), measurement builds only
+__device__ unsigned h9g_exact_wave[1 << 16];     // ... per wave (blockIdx * 4 + wave), pair kernel
 #endif
 namespace h9k {
 
@@ -1051,6 +1052,7 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
 #if defined(H9G_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)
     atomicAdd(&h9g_exact_count, 1ull);      // measurement builds only
+    atomicAdd(&h9g_exact_wave[(blockIdx.x * 4 + (threadIdx.x >> 6)) & 0xffff], 1u);
 #endif
     cs.launder();
     code = substep_exact_pair<L, G, CS>(&g, cs, T.exp2, T.log2);

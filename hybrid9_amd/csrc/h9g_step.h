@@ -134,15 +134,61 @@ struct MathExact {
   H9K_HD float powf(float x, float y) { return h9m::powf(x, y, T); }
   H9K_HD float div(float x, float d, double) { return x / d; }
 };
+// Out-of-line, cold: the exact re-run of a substep (h9g_pair.h).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define H9K_COLD __device__ __attribute__((noinline, cold))
+#else
+#define H9K_COLD static __attribute__((noinline, cold))
+#endif
+
+// glibc's full expf / powf, out of line: the in-place redo of MathFast
+// (rare), kept out of the hot loop's code and register allocation.
+H9K_COLD float expf_redo(float x, const uint64_t *e2, const double *l2) { return h9m::expf(x, {e2, l2}); }
+H9K_COLD float powf_redo(float x, float y, const uint64_t *e2, const double *l2) {
+  return h9m::powf(x, y, {e2, l2});
+}
+
 struct MathFast {
   static constexpr bool kExact = false;
   h9m::Tabs T;
-  bool special;
-  H9K_HD float expf(float x) { return h9m::expf_nx(x, T, special); }
-  H9K_HD float powf(float x, float y) { return h9m::powf_nx<false>(x, y, T, special); }
-  H9K_HD float div(float x, float, double r) {
-    const float q = (float)((double)x * r);
-    special |= bad_quotient(q);
+  bool special;             // set only by the water-table loops' third visit (visit_layers)
+  unsigned redone = 0;      // results redone in place (read by the self tests only)
+  // glibc's main path, branch-free; an input that glibc sends down another
+  // path (|x| >= 88 for expf; for powf x not a positive normal number or
+  // |y log2 x| >= 126, i.e. an under- or overflowing power such as the
+  // conductivity power of a very dry layer) is recomputed in place with
+  // glibc's full logic, in a branch that is rarely taken.  Round 1 re-ran
+  // the whole substep on the exact path for these inputs instead; a column
+  // that met one every substep made its wave, and so the kernel, up to
+  // 2.6x slower.
+  H9K_HD float expf(float x) {
+    bool sp = false;
+    float r = h9m::expf_nx(x, T, sp);
+    if (__builtin_expect(sp, 0)) {
+      r = expf_redo(x, T.exp2, T.log2);
+      redone++;
+    }
+    return r;
+  }
+  H9K_HD float powf(float x, float y) {
+    bool sp = false;
+    float r = h9m::powf_nx<false>(x, y, T, sp);
+    if (__builtin_expect(sp, 0)) {
+      r = powf_redo(x, y, T.exp2, T.log2);
+      redone++;
+    }
+    return r;
+  }
+  // x / d from the double reciprocal r: RN32(x * r) is the correctly rounded
+  // quotient whenever that is a normal or infinite float.  A
+  // subnormal quotient (the tiny fluxes of a very dry column) or a NaN one
+  // (d = 0, inf or NaN makes r NaN) is redone in place as the IEEE division.
+  H9K_HD float div(float x, float d, double r) {
+    float q = (float)((double)x * r);
+    if (__builtin_expect(bad_quotient(q), 0)) {
+      q = x / d;
+      redone++;
+    }
     return q;
   }
 };
@@ -361,11 +407,6 @@ H9K_HD Day make_day(float tas, float rlds, float rsds, float huss, float ps, flo
   return d;
 }
 
-// Out-of-line, cold: the exact re-run of a substep (h9g_pair.h).
-#if defined(__HIP_DEVICE_COMPILE__)
-#define H9K_COLD __device__ __attribute__((noinline, cold))
-#else
-#define H9K_COLD static __attribute__((noinline, cold))
-#endif
+
 
 }  // namespace h9k

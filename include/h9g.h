@@ -238,9 +238,14 @@ const char *h9g_kernel_name(h9g_ctx *ctx);
 /* out[i] = expf(x[i]) if y == NULL, else powf(x[i], y[i]), on device. */
 int h9g_math_selftest(int device, int n, const float *x, const float *y,
                       float *out);
+/* The same through the year kernels' math (glibc's main path; inputs that
+ * glibc sends down another path are redone in place with its full logic,
+ * flag[i] = 1 there). */
+int h9g_math_fast_selftest(int device, int n, const float *x, const float *y,
+                           float *out, int *flag);
 /* out[i] = x[i]/d[i] through the kernel's fast exact division (double
- * reciprocal); flag[i] = 1 where it defers to the exact path
- * (subnormal quotient). */
+ * reciprocal); flag[i] = 1 where the quotient was redone as
+ * the IEEE division (subnormal or NaN quotient). */
 int h9g_div_selftest(int device, int n, const float *x, const float *d,
                      float *out, int *flag);
 

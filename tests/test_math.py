@@ -57,6 +57,39 @@ def test_device_math_matches_glibc():
     assert same_bits(out, glibc_powf(x, y))
 
 
+@pytest.mark.gpu
+def test_device_fast_math_matches_glibc():
+    """The year kernels' math (MathFast): glibc's main path branch-free, and
+    every input glibc sends down another path (|x| >= 88 for expf; x not a
+    positive normal or |y log2 x| >= 126 for powf) redone in place -- equal
+    to glibc everywhere, including the under/overflowing powers of very dry
+    layers, which round 1 re-ran the whole substep for."""
+    import ctypes as C
+    import hybrid9_amd as h
+    lb = h.lib()
+    x, y = math_inputs()
+    # hot-path shaped underflowing powers: s1^(2b+2) with tiny s1, large b
+    rng = np.random.default_rng(9)
+    k = 1 << 18
+    xs = rng.uniform(1e-6, 0.05, k).astype(np.float32)
+    ys = rng.uniform(2.0, 25.0, k).astype(np.float32)
+    xe = rng.uniform(-110.0, -85.0, k).astype(np.float32)       # expf of deep water tables
+    px, py = np.concatenate([x, xs]), np.concatenate([y, ys])
+    ex = np.concatenate([x, xe])
+    out = np.empty_like(ex)
+    flag = np.empty(ex.size, np.int32)
+    fp = flag.ctypes.data_as(C.POINTER(C.c_int))
+    assert lb.h9g_math_fast_selftest(0, ex.size, h._fp(ex), None, h._fp(out), fp) == 0
+    assert same_bits(out, glibc_expf(ex))
+    assert flag[x.size:].sum() > 0.5 * k                            # took the redo branch
+    out = np.empty_like(px)
+    flag = np.empty(px.size, np.int32)
+    fp = flag.ctypes.data_as(C.POINTER(C.c_int))
+    assert lb.h9g_math_fast_selftest(0, px.size, h._fp(px), h._fp(py), h._fp(out), fp) == 0
+    assert same_bits(out, glibc_powf(px, py))
+    assert flag[x.size:].sum() > 0.1 * k
+
+
 def div_inputs(n=1 << 22, seed=5):
     """Dividends/divisors over the whole float range plus the cases that
     stress a reciprocal-based division: divisors near powers of two,
@@ -91,16 +124,16 @@ def test_device_fast_division_is_correctly_rounded():
     assert rc == 0
     with np.errstate(all="ignore"):
         ref = x / d
+    # exact everywhere; the subnormal quotients are the ones redone as x / d
+    assert same_bits(out, ref)
     sub = (ref != 0) & (np.abs(ref) < np.float32(2.0 ** -126))
     assert np.array_equal(flag.astype(bool), sub | ((out != 0) & (np.abs(out) < np.float32(2.0 ** -126))))
-    keep = flag == 0
-    assert same_bits(out[keep], ref[keep])
 
 
 @pytest.mark.gpu
 def test_device_fast_division_defers_on_zero_inf_nan_divisors():
-    """recip64 of 0, inf or NaN is NaN, so MathFast::div defers (the IEEE
-    quotient is inf, 0 or NaN there)."""
+    """recip64 of 0, inf or NaN is NaN, so MathFast::div redoes the quotient
+    as x / d (IEEE: inf, 0 or NaN there)."""
     import ctypes as C
     import hybrid9_amd as h
     d = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 0.0, np.inf], np.float32)
@@ -111,3 +144,5 @@ def test_device_fast_division_defers_on_zero_inf_nan_divisors():
                                   flag.ctypes.data_as(C.POINTER(C.c_int)))
     assert rc == 0
     assert flag.all()
+    with np.errstate(all="ignore"):
+        assert same_bits(out, x / d)
