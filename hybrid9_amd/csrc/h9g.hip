@@ -118,7 +118,8 @@ h9g_pair_kernel(const KArgs a, const G g) {
   const int n = a.ncell;
 
   PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1], (const lds_float *)s_zt,
-        a.sv + (size_t)blockIdx.x * (PS::GBLOCK / sizeof(float))};
+        a.sv + (size_t)blockIdx.x * (PS::GBLOCK / sizeof(float)),
+        (int)((blockIdx.x * 3u) / gridDim.x)};
   const Split2 sp{h};
   St<L> s;
 #pragma unroll
@@ -1248,6 +1249,50 @@ int h9g_sync(h9g_ctx *ctx) {
     fprintf(stderr, "h9g stamps (cycles/wave/substep):");
     for (int k = 0; k < 8; k++) { fprintf(stderr, " p%d=%.0f", k, sum[k] / steps); tot += sum[k]; }
     fprintf(stderr, " total=%.0f\n", tot / steps);
+    // load balance: per-wave totals (the kernel lasts as long as its slowest wave)
+    std::vector<double> wt(nw, 0.0);
+    for (size_t w = 0; w < nw; w++)
+      for (int k = 0; k < 8; k++) wt[w] += st[8 * w + k];
+    std::vector<double> ws(wt);
+    std::sort(ws.begin(), ws.end());
+    const double mean = tot / nw;
+    fprintf(stderr, "h9g wave totals / mean: min %.3f p50 %.3f p90 %.3f p99 %.3f max %.3f\n", ws[0] / mean,
+            ws[nw / 2] / mean, ws[nw * 9 / 10] / mean, ws[nw * 99 / 100] / mean, ws[nw - 1] / mean);
+    // by blockIdx % 8 (workgroups are dealt round-robin to the 8 XCDs) and by wave in block (SIMD)
+    double bx[8] = {0}, nx[8] = {0}, bs[4] = {0}, ns[4] = {0};
+    for (size_t w = 0; w < nw; w++) {
+      const size_t b = w / 4;
+      bx[b % 8] += wt[w];
+      nx[b % 8] += 1;
+      bs[w % 4] += wt[w];
+      ns[w % 4] += 1;
+    }
+    {  // phases of the slowest tenth of the waves against the fastest half
+      const double cut90 = ws[nw * 9 / 10], cut50 = ws[nw / 2];
+      double hi[8] = {0}, lo[8] = {0}, nh = 0, nl = 0;
+      for (size_t w = 0; w < nw; w++) {
+        if (wt[w] >= cut90) { nh++; for (int k = 0; k < 8; k++) hi[k] += st[8 * w + k]; }
+        if (wt[w] <= cut50) { nl++; for (int k = 0; k < 8; k++) lo[k] += st[8 * w + k]; }
+      }
+      const double sub = (double)days_in_year(ctx->last_year) * ctx->cfg.nisurf;
+      fprintf(stderr, "h9g slowest 10%% / fastest 50%% waves by phase (cycles/substep):");
+      for (int k = 0; k < 8; k++) fprintf(stderr, " p%d %.0f/%.0f", k, hi[k] / nh / sub, lo[k] / nl / sub);
+      fprintf(stderr, "\n");
+    }
+    {
+      fprintf(stderr, "h9g mean wave total by slot decile:");
+      for (int d = 0; d < 10; d++) {
+        double a = 0, c = 0;
+        for (size_t w = nw * d / 10; w < nw * (d + 1) / 10; w++) { a += wt[w]; c++; }
+        fprintf(stderr, " %.3f", a / c / mean);
+      }
+      fprintf(stderr, "\n");
+    }
+    fprintf(stderr, "h9g mean wave total by block%%8:");
+    for (int k = 0; k < 8; k++) fprintf(stderr, " %.3f", bx[k] / nx[k] / mean);
+    fprintf(stderr, "  by wave-in-block:");
+    for (int k = 0; k < 4; k++) fprintf(stderr, " %.3f", bs[k] / ns[k] / mean);
+    fprintf(stderr, "\n");
   }
 #endif
 #if defined(H9G_COUNT_EXACT)

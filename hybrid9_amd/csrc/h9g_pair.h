@@ -138,6 +138,7 @@ struct FlatStore {                     // host: one flat array per cell
   H9K_HD float sv_sc(int k) const { return sc(PS_SVZWT + k); }
   H9K_HD void sv_set_sc(int k, float v) const { set_sc(PS_SVZWT + k, v); }
   H9K_HD void sv_sync() const {}
+  H9K_HD void day_start(int) const {}
 };
 
 // Device: [row][S] LDS block per wave, S = lanes per wave.  Layer i of a
@@ -170,6 +171,25 @@ struct PairStore {
   lds_float *self, *even;
   const lds_float *zt;                 // zi(0..L+1), then zi(0..L+1)/1000 (per block)
   float *svw;                          // this workgroup's rollback block (global)
+  int round;                           // 0..2: which of the CU's three resident workgroups
+  // Issue fairness between the three waves of a SIMD (one from each of the
+  // CU's workgroups).  The SIMD arbitrates VALU issue by priority, then by
+  // wave age, so with equal priorities the oldest wave runs at its lone-wave
+  // rate, the youngest is starved, and the kernel ends on the youngest
+  // waves running alone (measured: the first-dispatched third of the waves
+  // took 0.82x the mean time, the last third 1.21x).  Rotating the top
+  // priority over the three rounds every day keeps them in step.
+  __device__ __forceinline__ void day_start(int day) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int p = (round + day) % 3;
+    if (p == 0)
+      __builtin_amdgcn_s_setprio(0);
+    else if (p == 1)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(2);
+#endif
+  }
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
   __device__ __forceinline__ double rdz_t(int i) const {
@@ -281,6 +301,7 @@ struct SoloStore {
   __device__ __forceinline__ float sv_sc(int k) const { return sc(PS_SVZWT + k); }
   __device__ __forceinline__ void sv_set_sc(int k, float v) const { set_sc(PS_SVZWT + k, v); }
   __device__ __forceinline__ void sv_sync() const {}
+  __device__ __forceinline__ void day_start(int) const {}
 };
 
 // Phase profiler (tools: H9G_STAMPS build only).  NoProf compiles away.
@@ -1101,6 +1122,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
   int code = 0;
   MathExact me{T};
   for (int day = 0; day < nt; day++) {
+    cs.day_start(day);
     cs.launder();
     opaque(A);
     const gbl_float *f = forc + (size_t)day * fday;
