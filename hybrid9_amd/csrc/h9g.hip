@@ -78,6 +78,9 @@ struct KArgs {
   unsigned *__restrict__ stamps;   // H9G_STAMPS builds: 8 phase cycle sums per wave
   float *__restrict__ sv;          // pair kernel: substep rollback, PairStore::GBLOCK bytes per workgroup
   const int *__restrict__ perm;    // lane slot -> cell (h9g_sort_kernel), or null: identity
+  unsigned *__restrict__ pace;     // pair kernel, Pacer mode 2: H9G_PACE_ROWS x 16 progress words
+  unsigned epoch;                  // Pacer mode 2: launch tag
+  int prio_mode;                   // Pacer mode: 0 none, 1 rotate, 2 pace
 };
 
 __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
@@ -117,9 +120,12 @@ h9g_pair_kernel(const KArgs a, const G g) {
   const int c = a.perm ? a.perm[slot] : slot;
   const int n = a.ncell;
 
+  int prow, pslot;
+  pace_key(prow, pslot);
   PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1], (const lds_float *)s_zt,
         a.sv + (size_t)blockIdx.x * (PS::GBLOCK / sizeof(float)),
-        (int)((blockIdx.x * 3u) / gridDim.x)};
+        Pacer{a.pace + (size_t)prow * 16, a.epoch & 0xfffffu, pslot, a.prio_mode,
+              (int)((blockIdx.x * (unsigned)PS::RESIDENT) / gridDim.x)}};
   const Split2 sp{h};
   St<L> s;
 #pragma unroll
@@ -712,6 +718,10 @@ struct h9g_ctx {
   int *d_slow = nullptr;
   float *d_sv = nullptr;          // pair kernel rollback blocks
   int *d_perm = nullptr;          // cell order of the year kernel (h9g_sort_kernel)
+  unsigned *d_pace = nullptr;     // Pacer mode 2 progress rows (h9g_pair.h)
+  unsigned epoch = 0;
+  int prio_mode = -1;             // H9G_PRIO: 0 none, 1 rotate, 2 pace; -1 auto (pace_mode)
+  int ncu = 256;
   int sort = 1;                   // H9G_SORT=0: identity order
   size_t sv_bytes = 0;
   int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel, 3: both (H9G_KERNEL=pair|solo|mixed; default by L)
@@ -805,6 +815,7 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_stamps);
   (void)hipFree(ctx->d_slow);
   (void)hipFree(ctx->d_perm);
+  (void)hipFree(ctx->d_pace);
   for (auto e : ctx->ev_copied) hipEventDestroy(e);
   for (auto e : ctx->ev_consumed) hipEventDestroy(e);
   for (int i = 0; i < NEVT; i++) {
@@ -962,10 +973,12 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
   // default: the pair kernel at L = 8; at L = 10 the kernel that needs less
   // time for this many columns (l10_kind)
   if (const char *se = getenv("H9G_SORT")) ctx->sort = atoi(se) != 0;
+  if (const char *se = getenv("H9G_PRIO")) ctx->prio_mode = atoi(se);
   const char *kenv = getenv("H9G_KERNEL");
   int ncu = 256;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1)
     ncu = 256;
+  ctx->ncu = ncu;
   if (kenv && strcmp(kenv, "solo") == 0)
     ctx->kind = 2;
   else if (kenv && strcmp(kenv, "pair") == 0)
@@ -1132,6 +1145,16 @@ static int join_prefetch(h9g_ctx *ctx, int slot) {
   return rc;
 }
 
+// Pacer mode of a pair launch over m cells (h9g_pair.h Pacer): pace when all
+// its workgroups are resident at once (one round), else rotate -- a wave of a
+// later round starts hundreds of days behind the waves it shares a SIMD with.
+static int pace_mode(const h9g_ctx *ctx, size_t m) {
+  if (ctx->prio_mode >= 0) return ctx->prio_mode;
+  const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
+  const size_t blocks = (m + per_block - 1) / per_block;
+  return blocks <= (size_t)ctx->ncu * (ctx->L <= 8 ? 3 : 2) ? 2 : 1;
+}
+
 int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   if (!ctx || slot < 0 || slot >= ctx->cfg.nslots || jyear < 1861 || jyear > 2299) return H9G_EINVAL;
   if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
@@ -1173,7 +1196,15 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
       ctx->sv_bytes = need;
     }
     a.sv = ctx->d_sv;
+    if (!ctx->d_pace) {
+      const size_t pb = sizeof(unsigned) * 16 * H9G_PACE_ROWS;
+      HIPCHK(hipMalloc(&ctx->d_pace, pb));
+      HIPCHK(hipMemsetAsync(ctx->d_pace, 0, pb, ctx->sc));
+    }
   }
+  a.pace = ctx->d_pace;
+  a.epoch = ++ctx->epoch;
+  a.prio_mode = pace_mode(ctx, ctx->kind == 3 ? ctx->n - ctx->n_solo : ctx->n);
 #if defined(H9G_STAMPS)
   if (!ctx->d_stamps) HIPCHK(hipMalloc(&ctx->d_stamps, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8)));
   HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8), ctx->sc));

@@ -155,6 +155,71 @@ struct FlatStore {                     // host: one flat array per cell
 // That leaves LDS room, within 3 workgroups per CU (76 rows per wave), for
 // the reciprocal fields: 1/(-psi) at any L, 1/theta_s and the day
 // reciprocals at L = 8 (76 rows; L = 10: 73 rows).
+// Issue priority of the waves sharing a SIMD (one from each of the CU's
+// resident workgroups).  The SIMD arbitrates VALU issue by priority, then by
+// wave age, so with equal priorities the oldest wave runs at its lone-wave
+// rate, the youngest is starved, and the kernel ends on the youngest waves
+// running alone (measured: the first-dispatched third of the waves took
+// 0.82x the mean time, the last third 1.21x).
+//   mode 1 (rotate): the top priority rotates over the resident rounds every
+//     day, so the waves get equal issue shares (config 2: 283 -> 251 ms;
+//     slowest wave 1.25 -> 1.09x the mean).  Rotating every 1, 4 or 16
+//     substeps instead measured the same.
+//   mode 2 (pace): each wave posts its day to a per-SIMD row in global memory
+//     (keyed by the hardware XCC/SE/SH/CU/SIMD ids, tagged with the launch
+//     epoch) and takes a priority equal to the number of waves on its SIMD
+//     that are ahead of it, so the waves of a SIMD keep the same day and
+//     finish together instead of one heavy wave finishing alone.
+struct Pacer {
+  unsigned *row;      // mode 2: this SIMD's 16 progress words
+  unsigned epoch;     // mode 2: launch tag (20 bits)
+  int me;             // mode 2: hardware wave slot (0..15)
+  int mode;
+  int round;          // mode 1: 0..resident-1, which of the CU's resident workgroups
+  __device__ __forceinline__ static void set_prio(int p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (p <= 0)
+      __builtin_amdgcn_s_setprio(0);
+    else if (p == 1)
+      __builtin_amdgcn_s_setprio(1);
+    else if (p == 2)
+      __builtin_amdgcn_s_setprio(2);
+    else
+      __builtin_amdgcn_s_setprio(3);
+#endif
+  }
+  __device__ __forceinline__ void day_start(int day, int resident) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (mode == 1) {
+      set_prio((round + day) % resident);
+    } else if (mode == 2) {
+      const unsigned mine = (epoch << 12) | (unsigned)(day + 1);
+      __hip_atomic_store(row + me, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int k = (int)(__lane_id() & 15);
+      const unsigned v = __hip_atomic_load(row + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool ahead = k != me && (v >> 12) == (epoch & 0xfffffu) && (v & 0xfffu) > (unsigned)(day + 1);
+      const uint64_t m = __builtin_amdgcn_ballot_w64(ahead);
+      const unsigned slots = (unsigned)(m | (m >> 16) | (m >> 32) | (m >> 48)) & 0xffffu;
+      set_prio(__builtin_popcount(slots));
+    }
+#endif
+  }
+};
+// Key of the SIMD this wave runs on and its slot there (HW_REG_HW_ID:
+// wave 3:0, simd 5:4, cu 11:8, sh 12, se 15:13; HW_REG_XCC_ID 3:0).
+#define H9G_PACE_ROWS 16384
+__device__ __forceinline__ void pace_key(int &row, int &slot) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+  slot = (int)(hw & 15u);
+  row = (int)(((((xcc * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) * 4u) +
+              ((hw >> 4) & 3u));
+#else
+  row = slot = 0;
+#endif
+}
+
 template <int L, int S>
 struct PairStore {
   static constexpr int NT = L / 2;
@@ -171,25 +236,9 @@ struct PairStore {
   lds_float *self, *even;
   const lds_float *zt;                 // zi(0..L+1), then zi(0..L+1)/1000 (per block)
   float *svw;                          // this workgroup's rollback block (global)
-  int round;                           // 0..2: which of the CU's three resident workgroups
-  // Issue fairness between the three waves of a SIMD (one from each of the
-  // CU's workgroups).  The SIMD arbitrates VALU issue by priority, then by
-  // wave age, so with equal priorities the oldest wave runs at its lone-wave
-  // rate, the youngest is starved, and the kernel ends on the youngest
-  // waves running alone (measured: the first-dispatched third of the waves
-  // took 0.82x the mean time, the last third 1.21x).  Rotating the top
-  // priority over the three rounds every day keeps them in step.
-  __device__ __forceinline__ void day_start(int day) const {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const int p = (round + day) % 3;
-    if (p == 0)
-      __builtin_amdgcn_s_setprio(0);
-    else if (p == 1)
-      __builtin_amdgcn_s_setprio(1);
-    else
-      __builtin_amdgcn_s_setprio(2);
-#endif
-  }
+  static constexpr int RESIDENT = L <= 8 ? 3 : 2;          // workgroups per CU = waves per SIMD (h9g.hip pair_waves)
+  Pacer pace;
+  __device__ __forceinline__ void day_start(int day) const { pace.day_start(day, RESIDENT); }
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
   __device__ __forceinline__ double rdz_t(int i) const {
