@@ -487,6 +487,23 @@ H9K_HD float divr(M &m, float x, float d, R rget) {
     return x / d;
 }
 
+// divr with the check deferred (MathFast::div_d): bad |= the quotient
+// needs the IEEE redo, done by divr_fix after the group.
+template <bool Use, class M, class R>
+H9K_HD float divr_d(M &m, float x, float d, R rget, bool &bad) {
+  if constexpr (Use) {
+    const float q = m.div_d(x, d, rget());
+    bad |= m.div_bad(q);
+    return q;
+  } else {
+    return x / d;
+  }
+}
+template <bool Use, class M>
+H9K_HD void divr_fix(M &m, float &q, float x, float d) {
+  if constexpr (Use) m.div_fix(q, x, d);
+}
+
 // Runs visit(k) for k = 0, 1, ... while it returns true (the reference's
 // layer loops with EXIT).  The fast path (MathFast) unrolls two visits --
 // the second only if some lane needs it -- and hands a third to the exact
@@ -578,10 +595,16 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
 
   // :141-151
   float w0 = DC(D_FORC) * dt + s.wa;
+  bool bad = false;                      // deferred checks (MathFast::div_d)
 #pragma unroll
   for (int i = 1; i <= L; i++) {
     w0 = w0 + h2o[i];
-    theta[i] = m.div(h2o[i], g.thk(i), g.rthk(i));
+    theta[i] = m.div_d(h2o[i], g.thk(i), g.rthk(i));
+    bad |= m.div_bad(theta[i]);
+  }
+  if (__builtin_expect(bad, 0)) {
+#pragma unroll
+    for (int i = 1; i <= L; i++) m.div_fix(theta[i], h2o[i], g.thk(i));
   }
   // :161-212
   const float qflx_top_soil = DC(D_FORC);
@@ -592,12 +615,25 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   const float frac_h2osfc = zero;
   // :269-276 (previous-step smp)
   float beta = zero;
+  {
+    float qb[L + 1];
+    bool badb = false;
 #pragma unroll
-  for (int i = 1; i <= L; i++) {
-    float b = one - m.div(smp[i] - g.zc(i), -150000.0f, 1.0 / -150000.0);
-    b = MINF(one, b);
-    b = MAXF(zero, b);
-    beta = beta + ROOT(i) * b;
+    for (int i = 1; i <= L; i++) {
+      qb[i] = m.div_d(smp[i] - g.zc(i), -150000.0f, 1.0 / -150000.0);
+      badb |= m.div_bad(qb[i]);
+    }
+    if (__builtin_expect(badb, 0)) {
+#pragma unroll
+      for (int i = 1; i <= L; i++) m.div_fix(qb[i], smp[i] - g.zc(i), -150000.0f);
+    }
+#pragma unroll
+    for (int i = 1; i <= L; i++) {
+      float b = one - qb[i];
+      b = MINF(one, b);
+      b = MAXF(zero, b);
+      beta = beta + ROOT(i) * b;
+    }
   }
   // :283-295
   float rsc;
@@ -690,15 +726,35 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
             auto rp = [&]() __attribute__((always_inline)) {
               return join_d(OWN(PF_RPSI0), OWN(PF_RPSI1));
             };
-            const float temp0 = m.powf(divr<CS::kRecip>(m, ((-psi) + zwtmm - zlo), -psi, rp), expo);
-            if ((zwtmm < zhi) && (zwtmm > zlo)) {
+            // temp0 and (below the layer) tempi are independent powers:
+            // both bases, then both powers, each pair checked once.  With the
+            // water table inside the layer tempi is not evaluated (its base
+            // is replaced by 1, whose power is exactly 1 and never special).
+            const bool inl = (zwtmm < zhi) && (zwtmm > zlo);
+            const float n0 = ((-psi) + zwtmm - zlo), ni = (-psi + zwtmm - zhi);
+            bool bq = false;
+            float b0 = divr_d<CS::kRecip>(m, n0, -psi, rp, bq);
+            float bi = divr_d<CS::kRecip>(m, ni, -psi, rp, bq);
+            if (__builtin_expect(bq, 0)) {
+              divr_fix<CS::kRecip>(m, b0, n0, -psi);
+              divr_fix<CS::kRecip>(m, bi, ni, -psi);
+            }
+            bi = inl ? one : bi;
+            bool s0, si;
+            float temp0 = m.powf_d(b0, expo, s0);
+            float tpi = m.powf_d(bi, expo, si);
+            if (__builtin_expect(s0 | si, 0)) {
+              m.powf_fix(temp0, b0, expo, s0);
+              m.powf_fix(tpi, bi, expo, si);
+            }
+            if (inl) {
               const float tempi = one;
               const float voleq1 = OWN(PF_PTE) / (zwtmm - zlo) * (tempi - temp0);
               vol_eq = m.div(voleq1 * (zwtmm - zlo) + ts * (zhi - zwtmm), zhi - zlo, cs.rdz_t(il));   // dz(i)
               vol_eq = MINF(ts, vol_eq);
               vol_eq = MAXF(vol_eq, zero);
             } else {
-              const float tempi = m.powf(divr<CS::kRecip>(m, (-psi + zwtmm - zhi), -psi, rp), expo);
+              const float tempi = tpi;
               vol_eq = OWN(PF_C3) * (tempi - temp0);
               vol_eq = MAXF(vol_eq, 0.0f);
               vol_eq = MINF(ts, vol_eq);
@@ -763,16 +819,25 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           float s1 = 0.5f * (th + thp) / (0.5f * (ts + tsp));
           s1 = MINF(one, s1);
           const float bsw = OWN(PF_BSW);
-          const float s2 = OWN(PF_HKS) * m.powf(s1, 2.0f * bsw + 2.0f);
-          FV<4> r;
-          r.v[0] = s1 * s2;
-          r.v[1] = (2.0f * bsw + 3.0f) * s2 * OWN(PF_ITS);
-          // (from the reciprocal only with room to spare in VGPRs: +35 spilled
-          // VGPRs at 168, measured)
+          // (s_node from the reciprocal only with room to spare in VGPRs: +35
+          // spilled VGPRs at 168, measured)
           float s_node = MAXF(divr<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }),
                               0.01f);
           s_node = MINF(one, s_node);
-          float sm = OWN(PF_PSI) * m.powf(s_node, -bsw);
+          // the two powers are independent: one deferred check
+          const float ek = 2.0f * bsw + 2.0f, es = -bsw;
+          bool sk, ss;
+          float pk = m.powf_d(s1, ek, sk);
+          float ps = m.powf_d(s_node, es, ss);
+          if (__builtin_expect(sk | ss, 0)) {
+            m.powf_fix(pk, s1, ek, sk);
+            m.powf_fix(ps, s_node, es, ss);
+          }
+          const float s2 = OWN(PF_HKS) * pk;
+          FV<4> r;
+          r.v[0] = s1 * s2;
+          r.v[1] = (2.0f * bsw + 3.0f) * s2 * OWN(PF_ITS);
+          float sm = OWN(PF_PSI) * ps;
           sm = MAXF(smpmin, sm);
           r.v[2] = sm;
           r.v[3] = (-bsw) * sm / (s_node * ts);
@@ -791,22 +856,46 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // bit for bit the same expressions, qin/dqidw0/dqidw1 of row k+1; they
   // are evaluated once.
   float dwat2[L + 2], GAM[L + 2];
-  float BET = zero, cprev = zero;
+  float BET = zero;
   double rbet = 0.0;
   int zero_pivot = 0;
+  // Row i also evaluates the next row's GAM(i+1) = c(i) / BET(i) (the
+  // reference's :827 of row i+1): it is independent of dwat2(i), so the two
+  // quotients share one deferred check.
   auto row = [&](int i, float am, float bm, float cm, float rm) __attribute__((always_inline)) {
+    float x;
     if (i == 1) {
       BET = bm;
-      rbet = recip64(BET);
-      dwat2[1] = m.div(rm, BET, rbet);
+      x = rm;
     } else {
-      GAM[i] = m.div(cprev, BET, rbet);
       BET = bm - am * GAM[i];
       if (BET == 0.0f && !zero_pivot) zero_pivot = i;
-      rbet = recip64(BET);
-      dwat2[i] = m.div(rm - am * dwat2[i - 1], BET, rbet);
+      x = rm - am * dwat2[i - 1];
     }
-    cprev = cm;
+    rbet = recip64(BET);
+    dwat2[i] = m.div_d(x, BET, rbet);
+    bool bad = m.div_bad(dwat2[i]);
+    if (i <= L) {
+      GAM[i + 1] = m.div_d(cm, BET, rbet);
+      bad |= m.div_bad(GAM[i + 1]);
+    }
+    if (__builtin_expect(bad, 0)) {
+      m.div_fix(dwat2[i], x, BET);
+      if (i <= L) m.div_fix(GAM[i + 1], cm, BET);
+    }
+  };
+  // qout, dqodw1, dqodw2 of one interface: independent quotients, one check.
+  auto flux3 = [&](float hki, float num, float dsi, float dsn, float dhk, float den, double rden, float &qo,
+                   float &d1, float &d2) __attribute__((always_inline)) {
+    const float x0 = -hki * num, x1 = -(-hki * dsi + num * dhk), x2 = -(hki * dsn + num * dhk);
+    qo = m.div_d(x0, den, rden);
+    d1 = m.div_d(x1, den, rden);
+    d2 = m.div_d(x2, den, rden);
+    if (__builtin_expect(m.div_bad(qo) | m.div_bad(d1) | m.div_bad(d2), 0)) {
+      m.div_fix(qo, x0, den);
+      m.div_fix(d1, x1, den);
+      m.div_fix(d2, x2, den);
+    }
   };
   float q_prev, dq0_prev, dq1_prev;      // interface i-1
   {
@@ -814,9 +903,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     const double rden = g.rden(1);
     const float dzq = (zq[2] - zq[1]);
     const float num = (smp[2] - smp[1]) - dzq;
-    const float qout = m.div(-hk[1] * num, den, rden);
-    const float dqodw1 = m.div(-(-hk[1] * dsmpdw[1] + num * dhkdw[1]), den, rden);
-    const float dqodw2 = m.div(-(hk[1] * dsmpdw[2] + num * dhkdw[1]), den, rden);
+    float qout, dqodw1, dqodw2;
+    flux3(hk[1], num, dsmpdw[1], dsmpdw[2], dhkdw[1], den, rden, qout, dqodw1, dqodw2);
     const float bm1 = m.div(g.dz(1), dt, g.rdt()) + dqodw1;
     if (bm1 == 0.0f) { errval = bm1; return 1; }                    // :806-812
     row(1, zero, bm1, dqodw2, qflx_infl - qout - tran * ROOT(1));
@@ -828,9 +916,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     const double rden = g.rden(i);
     const float dzq = zq[i + 1] - zq[i];
     const float num = (smp[i + 1] - smp[i]) - dzq;
-    const float qout = m.div(-hk[i] * num, den, rden);
-    const float dqodw1 = m.div(-(-hk[i] * dsmpdw[i] + num * dhkdw[i]), den, rden);
-    const float dqodw2 = m.div(-(hk[i] * dsmpdw[i + 1] + num * dhkdw[i]), den, rden);
+    float qout, dqodw1, dqodw2;
+    flux3(hk[i], num, dsmpdw[i], dsmpdw[i + 1], dhkdw[i], den, rden, qout, dqodw1, dqodw2);
     row(i, -dq0_prev, m.div(g.dz(i), dt, g.rdt()) - dq1_prev + dqodw1, dqodw2,
         q_prev - qout - tran * ROOT(i));
     q_prev = qout; dq0_prev = dqodw1; dq1_prev = dqodw2;
@@ -847,9 +934,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
       const double rden = recip64(den);
       const float dzq = zq[i + 1] - zq[i];
       const float num = smp1 - smp[i] - dzq;
-      const float qout = m.div(-hk[i] * num, den, rden);
-      const float dqodw1 = m.div(-(-hk[i] * dsmpdw[i] + num * dhkdw[i]), den, rden);
-      const float dqodw2 = m.div(-(hk[i] * dsmpdw1 + num * dhkdw[i]), den, rden);
+      float qout, dqodw1, dqodw2;
+      flux3(hk[i], num, dsmpdw[i], dsmpdw1, dhkdw[i], den, rden, qout, dqodw1, dqodw2);
       row(i, -dq0_prev, m.div(g.dz(i), dt, g.rdt()) - dq1_prev + dqodw1, dqodw2,
           q_prev - qout - tran * ROOT(i));
       const float qout1 = zero, dqodw1b = zero;

@@ -133,6 +133,15 @@ struct MathExact {
   H9K_HD float expf(float x) { return h9m::expf(x, T); }
   H9K_HD float powf(float x, float y) { return h9m::powf(x, y, T); }
   H9K_HD float div(float x, float d, double) { return x / d; }
+  // deferred-check forms (MathFast): nothing to defer, never flagged
+  H9K_HD float powf_d(float x, float y, bool &sp) {
+    sp = false;
+    return h9m::powf(x, y, T);
+  }
+  H9K_HD void powf_fix(float &, float, float, bool) {}
+  H9K_HD float div_d(float x, float d, double) { return x / d; }
+  H9K_HD bool div_bad(float) const { return false; }
+  H9K_HD void div_fix(float &, float, float) {}
 };
 // Out-of-line, cold: the exact re-run of a substep (h9g_pair.h).
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -190,6 +199,32 @@ struct MathFast {
       redone++;
     }
     return q;
+  }
+  // Deferred checks.  A per-operation "redo if special" branch ends the
+  // basic block, so the scheduler cannot interleave independent powers or
+  // quotients and every one runs at its full dependency latency.  The _d
+  // forms evaluate branch-free; a group of independent operations is then
+  // followed by ONE rarely-taken branch (any flag set) in which _fix redoes
+  // exactly the flagged results, as powf/div above would have:
+  //   float a = m.powf_d(x0, y0, s0), b = m.powf_d(x1, y1, s1);
+  //   if (__builtin_expect(s0 | s1, 0)) { m.powf_fix(a, x0, y0, s0); ... }
+  H9K_HD float powf_d(float x, float y, bool &sp) {
+    sp = false;
+    return h9m::powf_nx<false>(x, y, T, sp);
+  }
+  H9K_HD void powf_fix(float &r, float x, float y, bool sp) {
+    if (sp) {
+      r = powf_redo(x, y, T.exp2, T.log2);
+      redone++;
+    }
+  }
+  H9K_HD float div_d(float x, float, double r) { return (float)((double)x * r); }
+  H9K_HD bool div_bad(float q) const { return bad_quotient(q); }
+  H9K_HD void div_fix(float &q, float x, float d) {
+    if (bad_quotient(q)) {
+      q = x / d;
+      redone++;
+    }
   }
 };
 
