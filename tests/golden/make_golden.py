@@ -297,6 +297,43 @@ def l10_case(name="c5_l10_sample", year0=1901, nyears=2, nisurf=24):
     print(f"{name}: {n} cells x {nyears} yr, STOPs {stops}, {(OUT / f'{name}.npz').stat().st_size / 1e3:.0f} kB")
 
 
+def bench_stop_case(name="c2_bench_stop", year0=1901, nyears=10, nisurf=48):
+    """The config-2 bench's own STOP.  Over the driver's years (1901-1925,
+    seed SEED, GROW off) one of the 67,420 synthetic land cells reaches the
+    water-imbalance STOP (HYDROLOGY.f90:1244) in 1910: land index 20735,
+    gid 53140, found on the GPU by tools/find_stops.py
+    (profiles/stops_config2_r02.json).  The reference runs that cell alone
+    from 1901 and must STOP at the same place; three other cells of the
+    same grid run alongside it in a second reference run and must not."""
+    land = synth.land_cells()
+    stop_idx, other = 20735, [20734, 20736, 41000]
+    idx = other + [stop_idx]
+    gid = land[idx].astype(np.int64)
+    p, f = synth_inputs(gid, year0, nyears)
+    n = gid.size
+    ok = np.arange(n) < len(other)
+    sub = lambda a: {k: v[ok] for k, v in a.items()}  # noqa: E731
+    out = refcase.run_case(zi=synth.ZI_L8, params=sub(p), forcing=np.ascontiguousarray(f[:, :, ok]),
+                           nisurf=nisurf, year0=year0, nyears=nyears, grow_on=0)
+    annual = np.full((nyears, 20, n), np.nan, np.float32)
+    annual[:, :, ok] = out["annual"]
+    one = {k: v[n - 1:] for k, v in p.items()}
+    try:
+        refcase.run_case(zi=synth.ZI_L8, params=one, forcing=np.ascontiguousarray(f[:, :, n - 1:]),
+                         nisurf=nisurf, year0=year0, nyears=nyears, grow_on=0)
+    except refcase.RefStop as e:
+        stops = [dict(e.info, cell=n - 1)]
+    else:
+        raise SystemExit(f"{name}: land cell {stop_idx} was expected to STOP")
+    meta = dict(name=name, kind="bench_stop", seed=synth.SEED, gid=gid.tolist(), L=8, ncell=int(n),
+                year0=year0, nyears=nyears, nisurf=nisurf, grow_on=0, zi=synth.ZI_L8.tolist(), stops=stops,
+                input_sha256=digest(packed_params(p), f),
+                generator="oracle/_ref/h9ref (reference HYDROLOGY.f90/GROW.f90, amdflang -O2)")
+    np.savez_compressed(OUT / f"{name}.npz", meta=np.array(json.dumps(meta)), annual=annual,
+                        state_ok=refcase.pack_state(out["state"], 8), ok=ok)
+    print(f"{name}: {n} cells x {nyears} yr, STOPs {stops}")
+
+
 def site_inputs(gid, L, nisurf, years, events, seed=synth.SEED, soils="synth", ppt_scale=1.0):
     """Synthetic LCLIM site inputs (hybrid9_amd.site): soils of the land
     cells gid (soils="independent": independent_layer_params), site forcing
@@ -380,6 +417,7 @@ def main():
     main_lclim()
     spinup_case()
     l10_case()
+    bench_stop_case()
 
 
 if __name__ == "__main__":

@@ -94,6 +94,30 @@ def test_config5_l10_matches_reference_golden(kernel, monkeypatch):
     assert same_bits(refcase.pack_state(st, meta["L"]), exp["state_ok"])
 
 
+@pytest.mark.parametrize("kernel", ["pair", "solo"])
+def test_gpu_reproduces_bench_stop(kernel, monkeypatch):
+    """The config-2 bench's own STOP (land cell 20735 reaches the
+    water-imbalance STOP on day 92 of 1910 in the driver's run): the product
+    path over 1901-1910 stops that cell where the reference does, with the
+    reference's record, and the three other cells match it bit for bit."""
+    monkeypatch.setenv("H9G_KERNEL", kernel)
+    meta, inp, exp = load_golden("c2_bench_stop")
+    ok = exp["ok"]
+    out = h.run(zi=inp["zi"], params=inp["params"], forcing=inp["forcing"], nisurf=inp["nisurf"],
+                year0=inp["year0"], nyears=inp["nyears"], grow_on=False, stop_on_error=False)
+    (s,) = meta["stops"]
+    c = s["cell"]
+    e = out["errors"]
+    assert np.array_equal(np.nonzero(e["code"])[0], [c])
+    assert (e["code"][c], e["day"][c]) == (s["code"], s["day"])
+    assert e["value"][c] == np.float32(s["value"])                 # printed by the reference to 8 digits
+    assert out["err"]["year"] == meta["year0"] + meta["nyears"] - 1
+    assert same_bits(out["annual"][:, :, ok], exp["annual"][:, :, ok])
+    st = refcase.unpack_state(out["state"], meta["ncell"], meta["L"])
+    st = {k: v[ok] for k, v in st.items()}
+    assert same_bits(refcase.pack_state(st, meta["L"]), exp["state_ok"])
+
+
 def test_reference_stop_raises():
     meta, inp, _ = load_golden("stop_ns24")
     n = meta["ncell"]

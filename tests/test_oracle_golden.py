@@ -63,3 +63,23 @@ def test_oracle_matches_reference_l10_golden():
     assert f"{out['err']['value']:.9g}" == f"{s['value']:.9g}"
     st = {k: (v[ok] if v.ndim else v) for k, v in out["state"].items()}
     assert same_bits(refcase.pack_state(st, L), exp["state_ok"])
+
+
+def test_oracle_reproduces_bench_stop():
+    """The config-2 bench's own STOP (land cell 20735, 1910, found by the
+    GPU run of the driver's years; tests/golden make_golden.bench_stop_case):
+    the reference STOPs there, and so does the oracle, with the same record;
+    three cells of the same grid run through the 10 years bit for bit."""
+    meta, inp, exp = load_golden("c2_bench_stop")
+    ok = exp["ok"]
+    out = port.run(zi=inp["zi"], params=inp["params"], forcing=inp["forcing"], nisurf=inp["nisurf"],
+                   year0=inp["year0"], nyears=inp["nyears"], grow_on=inp["grow_on"], nthreads=4)
+    (s,) = meta["stops"]
+    c = s["cell"]
+    assert out["rc"] == s["code"] and out["err"]["cell"] == c
+    assert out["errors"]["code"][c] == s["code"] and out["errors"]["day"][c] == s["day"]
+    assert out["errors"]["value"][c] == np.float32(s["value"])     # printed by the reference to 8 digits
+    assert np.array_equal(np.nonzero(out["errors"]["code"])[0], [c])
+    assert same_bits(out["annual"][:, :, ok], exp["annual"][:, :, ok])
+    st = {k: (v[ok] if v.ndim else v) for k, v in out["state"].items()}
+    assert same_bits(refcase.pack_state(st, meta["L"]), exp["state_ok"])
