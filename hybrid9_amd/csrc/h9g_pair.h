@@ -69,6 +69,13 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
                   (PS_DAY + D_DRR) % 2 == 0 && (PS_DAY + D_RAC) % 2 == 0 && PS_DR0 % 2 == 0,
               "pair fields must start a row");
 
+#ifndef H9G_FE_EQ
+#define H9G_FE_EQ 1   // fence interval of the equilibrium-profile slots (Split2::par)
+#endif
+#ifndef H9G_FE_HK
+#define H9G_FE_HK 1   // ... of the conductivity / matric-potential slots
+#endif
+
 template <int K>
 struct FV {
   float v[K];
@@ -391,13 +398,31 @@ struct SplitAll {
   template <class CS>
   H9K_HD float own(const CS &cs, int p, int t, int h) const { return cs.lay(p, 2 * t + 1 + h); }
   // out[2t+1+h] = f(t, h).f for every layer; K outputs per layer
-  template <int NT, int K, class F>
+  template <int NT, int K, int FE = 1, class F>
   H9K_HD void par(F f, float *const (&out)[K]) const {
 #pragma unroll
     for (int t = 0; t < NT; t++) {
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const FV<K> r = f(t, h);
+#pragma unroll
+        for (int k = 0; k < K; k++) out[k][2 * t + 1 + h] = r.v[k];
+      }
+      sched_fence();
+    }
+  }
+  // par with deferred checks: fast(t, h, bad) is branch-free and sets bad
+  // when any of its results needs glibc's/IEEE's other path; exact(t, h)
+  // (the body with in-place redos) then recomputes the layer.
+  template <int NT, int K, int FE = 1, class FF, class FX>
+  H9K_HD void par_d(FF fast, FX exact, float *const (&out)[K]) const {
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        bool bad = false;
+        FV<K> r = fast(t, h, bad);
+        if (bad) r = exact(t, h);
 #pragma unroll
         for (int k = 0; k < K; k++) out[k][2 * t + 1 + h] = r.v[k];
       }
@@ -423,7 +448,9 @@ struct Split2 {
   int h;
   template <class CS>
   H9K_HD float own(const CS &cs, int p, int t, int) const { return cs.slot(p, t); }
-  template <int NT, int K, class F>
+  // FE: a scheduling fence after every FE slots (FE > 1 lets the scheduler
+  // interleave FE slots' powers, at FE times the live temporaries)
+  template <int NT, int K, int FE = 1, class F>
   H9K_HD void par(F f, float *const (&out)[K]) const {
 #pragma unroll
     for (int t = 0; t < NT; t++) {
@@ -434,7 +461,34 @@ struct Split2 {
         out[k][2 * t + 1] = sel(h, r.v[k], o);
         out[k][2 * t + 2] = sel(h, o, r.v[k]);
       }
-      sched_fence();
+      if ((t + 1) % FE == 0 || t == NT - 1) sched_fence();
+    }
+  }
+  // par with the special-case checks of all NT slots deferred to one
+  // rarely-taken branch after them (SplitAll::par_d): with no per-slot
+  // branch the slots form one basic block, so the scheduler can interleave
+  // FE slots' powers.  A lane with any flag recomputes its slots exactly.
+  template <int NT, int K, int FE = 1, class FF, class FX>
+  H9K_HD void par_d(FF fast, FX exact, float *const (&out)[K]) const {
+    FV<K> r[NT];
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      r[t] = fast(t, h, bad);
+      if ((t + 1) % FE == 0 || t == NT - 1) sched_fence();
+    }
+    if (__builtin_expect(bad, 0)) {
+#pragma unroll
+      for (int t = 0; t < NT; t++) r[t] = exact(t, h);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const float o = pair_swap(r[t].v[k]);
+        out[k][2 * t + 1] = sel(h, r[t].v[k], o);
+        out[k][2 * t + 2] = sel(h, o, r[t].v[k]);
+      }
     }
   }
   template <int K, class F>
@@ -712,8 +766,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   float zq[L + 2];
   {
     float *const out[1] = {zq};
-    sp.template par<NT, 1>(
-        [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
+    // exact: the reference expression with every special case redone in place
+    auto eq_exact = [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
           const int i0 = 2 * t + 1;                           // own layer il = i0 + h
           const int il = i0 + h;
           const float zlo = cs.zi(il - 1), zhi = cs.zi(il);   // zi(i-1), zi(i): geometry table
@@ -763,8 +817,48 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           const float qv = divr<CS::kRts>(m, vol_eq, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); });
           float z = psi * m.powf(MAXF(qv, 0.01f), -OWN(PF_BSW));
           return FV<1>{{MAXF(smpmin, z)}};
-        },
-        out);
+    };
+    // fast: the same values branch-free (all three cases evaluated, the
+    // layer's selected); bad = some quotient or power of the selected case
+    // needs its other path (then eq_exact recomputes the slot).  Bases of
+    // cases not taken are replaced by 1 so they raise no flag.
+    auto eq_fast = [&](int t, int h, bool &bad) __attribute__((always_inline)) -> FV<1> {
+          const int il = 2 * t + 1 + h;
+          const float zlo = cs.zi(il - 1), zhi = cs.zi(il);
+          const float ts = OWN(PF_TS), psi = OWN(PF_PSI);
+          const bool sat = zwtmm <= zlo;
+          const bool inl = (zwtmm < zhi) && (zwtmm > zlo);
+          const float expo = one + OWN(PF_NINVB);
+          const double rp = join_d(OWN(PF_RPSI0), OWN(PF_RPSI1));
+          const float n0 = ((-psi) + zwtmm - zlo), ni = (-psi + zwtmm - zhi);
+          float b0 = divr_d<CS::kRecip>(m, n0, -psi, [&]() { return rp; }, bad);
+          float bi = divr_d<CS::kRecip>(m, ni, -psi, [&]() { return rp; }, bad);
+          b0 = sat ? one : b0;
+          bi = (sat || inl) ? one : bi;
+          bool s0, si;
+          const float temp0 = m.powf_d(b0, expo, s0);
+          const float tpi = m.powf_d(bi, expo, si);
+          bad |= s0 | si;
+          // water table inside the layer (:530-543)
+          const float d0 = zwtmm - zlo;
+          const float q1 = m.div_d(OWN(PF_PTE), d0, recip64(d0));
+          const float voleq1 = q1 * (one - temp0);
+          float vin = m.div_d(voleq1 * (zwtmm - zlo) + ts * (zhi - zwtmm), zhi - zlo, cs.rdz_t(il));
+          bad |= inl && (m.div_bad(q1) | m.div_bad(vin));
+          vin = MINF(ts, vin);
+          vin = MAXF(vin, zero);
+          // water table below the layer (:548-558)
+          float vbl = OWN(PF_C3) * (tpi - temp0);
+          vbl = MAXF(vbl, 0.0f);
+          vbl = MINF(ts, vbl);
+          const float vol_eq = sat ? ts : (inl ? vin : vbl);
+          const float qv = divr_d<CS::kRts>(m, vol_eq, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }, bad);
+          bool sz;
+          const float z = psi * m.powf_d(MAXF(qv, 0.01f), -OWN(PF_BSW), sz);
+          bad |= sz;
+          return FV<1>{{MAXF(smpmin, z)}};
+    };
+    sp.template par_d<NT, 1, H9G_FE_EQ>(eq_fast, eq_exact, out);
   }
   // Four single powers split over the pair (unused ones get base 1):
   //   lane 0: temp0 of the aquifer node (:579-580), then zq(L+1) (:581-590);
@@ -808,8 +902,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   float hk[L + 1], dhkdw[L + 1], dsmpdw[L + 1];
   {
     float *const out[4] = {hk, dhkdw, smp, dsmpdw};
-    sp.template par<NT, 4>(
-        [&](int t, int h) __attribute__((always_inline)) -> FV<4> {
+    auto hk_exact = [&](int t, int h) __attribute__((always_inline)) -> FV<4> {
           const int i0 = 2 * t + 1;
           const int ip1 = (L < i0 + 2) ? L : i0 + 2;          // ip of layer i0+1
           const float th = sel(h, theta[i0], theta[i0 + 1]);
@@ -842,8 +935,37 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           r.v[2] = sm;
           r.v[3] = (-bsw) * sm / (s_node * ts);
           return r;
-        },
-        out);
+    };
+    // the same, branch-free, flags deferred (par_d)
+    auto hk_fast = [&](int t, int h, bool &bad) __attribute__((always_inline)) -> FV<4> {
+          const int i0 = 2 * t + 1;
+          const int ip1 = (L < i0 + 2) ? L : i0 + 2;
+          const float th = sel(h, theta[i0], theta[i0 + 1]);
+          const float thp = sel(h, theta[i0 + 1], theta[ip1]);
+          const float ts = OWN(PF_TS);
+          const float tsp = sel(h, TS(i0 + 1), TS(ip1));
+          float s1 = 0.5f * (th + thp) / (0.5f * (ts + tsp));
+          s1 = MINF(one, s1);
+          const float bsw = OWN(PF_BSW);
+          float s_node = MAXF(divr_d<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }, bad),
+                              0.01f);
+          s_node = MINF(one, s_node);
+          const float ek = 2.0f * bsw + 2.0f, es = -bsw;
+          bool sk, ss;
+          const float pk = m.powf_d(s1, ek, sk);
+          const float ps = m.powf_d(s_node, es, ss);
+          bad |= sk | ss;
+          const float s2 = OWN(PF_HKS) * pk;
+          FV<4> r;
+          r.v[0] = s1 * s2;
+          r.v[1] = (2.0f * bsw + 3.0f) * s2 * OWN(PF_ITS);
+          float sm = OWN(PF_PSI) * ps;
+          sm = MAXF(smpmin, sm);
+          r.v[2] = sm;
+          r.v[3] = (-bsw) * sm / (s_node * ts);
+          return r;
+    };
+    sp.template par_d<NT, 4, H9G_FE_HK>(hk_fast, hk_exact, out);
   }
   pr.mark(3);
   // :645-650 aquifer node geometry
