@@ -558,6 +558,16 @@ H9K_HD void divr_fix(M &m, float &q, float x, float d) {
   if constexpr (Use) m.div_fix(q, x, d);
 }
 
+// expf on glibc's main path, flagged (sp) when glibc takes another path
+// (then M::expf recomputes); MathExact computes it exactly, never flagged.
+template <class M>
+H9K_HD float expf_fast(M &m, float x, bool &sp) {
+  if constexpr (M::kExact)
+    return m.expf(x);
+  else
+    return h9m::expf_nx(x, m.T, sp);
+}
+
 // Runs visit(k) for k = 0, 1, ... while it returns true (the reference's
 // layer loops with EXIT).  The fast path (MathFast) unrolls two visits --
 // the second only if some lane needs it -- and hands a third to the exact
@@ -1203,8 +1213,17 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     FV<1> pK, pS;
     sp.template pick<1>(
         [&](int h) __attribute__((always_inline)) -> FV<1> {
-          const float b = h ? s_y_base(jwt + 1, zwtmm) : s1;
-          return FV<1>{{m.powf(b, sel(h, 2.0f * bsw_j + 3.0f, cs.lay(PF_NINVB, jwt + 1)))}};
+          const int j1 = jwt + 1;
+          const float nb = -cs.lay(PF_PSI, j1);
+          bool sq = false, sw = false;
+          float q = divr_d<CS::kRecip>(m, zwtmm, nb, [&]() { return lay_d(cs, PF_RPSI0, j1); }, sq);
+          const float e = sel(h, 2.0f * bsw_j + 3.0f, cs.lay(PF_NINVB, j1));
+          float w = m.powf_d(h ? one + q : s1, e, sw);
+          if (__builtin_expect((h && sq) | sw, 0)) {          // one deferred check
+            divr_fix<CS::kRecip>(m, q, zwtmm, nb);
+            w = m.powf(h ? one + q : s1, e);
+          }
+          return FV<1>{{w}};
         },
         pK, pS);
     sy_first = s_y_of(jwt + 1, pS.v[0]);
@@ -1264,13 +1283,26 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // :1015-1035 baseflow; s_y(L) for the new zwtmm (:1077-1080) on one lane
   // of the pair, the drainage loop's first layer s_y(jwt2+1) on the other
   zwtmm = 1000.0f * s.zwt;
-  float rsub_top = 5.5E-3f * m.expf(-fff * s.zwt);
+  // rsub_top's exponential and the pair's power are independent: both
+  // branch-free, one deferred check (before the pair exchange).
+  float rsub_top;
   const int jd = jwt2 < L ? jwt2 + 1 : L;
   FV<1> pR, pD;
   sp.template pick<1>(
       [&](int h) __attribute__((always_inline)) -> FV<1> {
         const int i = h ? jd : L;
-        return FV<1>{{m.powf(s_y_base(i, zwtmm), cs.lay(PF_NINVB, i))}};
+        bool se = false, sq = false, sw = false;
+        float ex = expf_fast(m, -fff * s.zwt, se);
+        const float nb = -cs.lay(PF_PSI, i);
+        float q = divr_d<CS::kRecip>(m, zwtmm, nb, [&]() { return lay_d(cs, PF_RPSI0, i); }, sq);
+        float w = m.powf_d(one + q, cs.lay(PF_NINVB, i), sw);
+        if (__builtin_expect(se | sq | sw, 0)) {
+          if (se) ex = m.expf(-fff * s.zwt);
+          divr_fix<CS::kRecip>(m, q, zwtmm, nb);
+          w = m.powf(one + q, cs.lay(PF_NINVB, i));
+        }
+        rsub_top = 5.5E-3f * ex;
+        return FV<1>{{w}};
       },
       pR, pD);
   rous = s_y_of(L, pR.v[0]);
