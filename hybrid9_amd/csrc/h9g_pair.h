@@ -892,12 +892,23 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     ve = MINF(TS(L), ve);
     sp.template pick<2>(
         [&](int h) __attribute__((always_inline)) -> FV<2> {
-          const float q2 = divr<CS::kRts>(m, sel(h, ve, theta[L]), TS(L), [&]() { return lay_d(cs, PF_RTS0, L); });
-          float sn = MAXF(0.5f * (one + q2), 0.01f);
-          sn = MINF(one, sn);
-          float x = sel(h, MAXF(q2, 0.01f), sn);
-          if (!aq) x = one;
-          float z = PSI(L) * m.powf(x, -BSW(L));
+          const float xn = sel(h, ve, theta[L]);
+          auto xof = [&](float q2) __attribute__((always_inline)) {
+            float sn = MAXF(0.5f * (one + q2), 0.01f);
+            sn = MINF(one, sn);
+            const float x = sel(h, MAXF(q2, 0.01f), sn);
+            return aq ? x : one;
+          };
+          bool sq = false, sw = false;        // one deferred check for the quotient and the power
+          float q2 = divr_d<CS::kRts>(m, xn, TS(L), [&]() { return lay_d(cs, PF_RTS0, L); }, sq);
+          float x = xof(q2);
+          float pw = m.powf_d(x, -BSW(L), sw);
+          if (__builtin_expect(sq | sw, 0)) {
+            divr_fix<CS::kRts>(m, q2, xn, TS(L));
+            x = xof(q2);
+            pw = m.powf(x, -BSW(L));
+          }
+          float z = PSI(L) * pw;
           z = MAXF(smpmin, z);
           return FV<2>{{z, -BSW(L) * z / (x * TS(L))}};
         },
