@@ -1219,20 +1219,21 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
       if (i == jwt) zc_j = g.zc(i);
     }
     const float wh_zwt = zero;
-    const float s_node = MAXF(th_j / ts_j, 0.01f);
-    const float s1 = MINF(one, s_node);
     FV<1> pK, pS;
     sp.template pick<1>(
         [&](int h) __attribute__((always_inline)) -> FV<1> {
           const int j1 = jwt + 1;
           const float nb = -cs.lay(PF_PSI, j1);
-          bool sq = false, sw = false;
+          bool st = false, sq = false, sw = false;
+          float tq = th_j / ts_j;
+          auto s1of = [&](float t) __attribute__((always_inline)) { return MINF(one, MAXF(t, 0.01f)); };
           float q = divr_d<CS::kRecip>(m, zwtmm, nb, [&]() { return lay_d(cs, PF_RPSI0, j1); }, sq);
           const float e = sel(h, 2.0f * bsw_j + 3.0f, cs.lay(PF_NINVB, j1));
-          float w = m.powf_d(h ? one + q : s1, e, sw);
-          if (__builtin_expect((h && sq) | sw, 0)) {          // one deferred check
+          float w = m.powf_d(h ? one + q : s1of(tq), e, sw);
+          if (__builtin_expect((h ? sq : st) | sw, 0)) {      // one deferred check
+            divr_fix<CS::kRts>(m, tq, th_j, ts_j);
             divr_fix<CS::kRecip>(m, q, zwtmm, nb);
-            w = m.powf(h ? one + q : s1, e);
+            w = m.powf(h ? one + q : s1of(tq), e);
           }
           return FV<1>{{w}};
         },
@@ -1367,7 +1368,16 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // :1144-1152
   const float xs1 = MAXF(MAXF(h2o[1], zero) - cs.sc(PS_TSDZ1), zero);
   h2o[1] = MINF(cs.sc(PS_TSDZ1), h2o[1]);
-  const float qflx_rsub_sat = m.div(xs1, dt, g.rdt());
+  float qflx_rsub_sat = m.div_d(xs1, dt, g.rdt());   // checked with the watmin section's branch
+  // :1161-1211 watmin.  With no layer below watmin every xs is zero and
+  // every update below is an identity (x + 0 would change only x = -0, and
+  // -0 < watmin), so a lane with no layer below watmin skips the section:
+  // one rarely-taken branch instead of one per layer.
+  bool low = false;
+#pragma unroll
+  for (int i = 1; i <= L; i++) low |= h2o[i] < watmin;
+  if (__builtin_expect(low | m.div_bad(qflx_rsub_sat), 0)) {
+  m.div_fix(qflx_rsub_sat, xs1, dt);
   // :1161-1174 watmin top-down
 #pragma unroll
   for (int i = 1; i <= L - 1; i++) {
@@ -1403,6 +1413,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   }
   h2o[L] = h2o[L] + xs;
   rsub_top = rsub_top - m.div(xs, dt, g.rdt());
+  }  // low
   // :1221-1236.  The end-of-step theta (:1233) is read only by the daily
   // sums after the day's last substep (the next substep recomputes theta
   // from h2osoi_liq, :141-151), so cell_year_pair evaluates it once a day.
