@@ -892,23 +892,12 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     ve = MINF(TS(L), ve);
     sp.template pick<2>(
         [&](int h) __attribute__((always_inline)) -> FV<2> {
-          const float xn = sel(h, ve, theta[L]);
-          auto xof = [&](float q2) __attribute__((always_inline)) {
-            float sn = MAXF(0.5f * (one + q2), 0.01f);
-            sn = MINF(one, sn);
-            const float x = sel(h, MAXF(q2, 0.01f), sn);
-            return aq ? x : one;
-          };
-          bool sq = false, sw = false;        // one deferred check for the quotient and the power
-          float q2 = divr_d<CS::kRts>(m, xn, TS(L), [&]() { return lay_d(cs, PF_RTS0, L); }, sq);
-          float x = xof(q2);
-          float pw = m.powf_d(x, -BSW(L), sw);
-          if (__builtin_expect(sq | sw, 0)) {
-            divr_fix<CS::kRts>(m, q2, xn, TS(L));
-            x = xof(q2);
-            pw = m.powf(x, -BSW(L));
-          }
-          float z = PSI(L) * pw;
+          const float q2 = divr<CS::kRts>(m, sel(h, ve, theta[L]), TS(L), [&]() { return lay_d(cs, PF_RTS0, L); });
+          float sn = MAXF(0.5f * (one + q2), 0.01f);
+          sn = MINF(one, sn);
+          float x = sel(h, MAXF(q2, 0.01f), sn);
+          if (!aq) x = one;
+          float z = PSI(L) * m.powf(x, -BSW(L));
           z = MAXF(smpmin, z);
           return FV<2>{{z, -BSW(L) * z / (x * TS(L))}};
         },
@@ -1219,21 +1208,20 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
       if (i == jwt) zc_j = g.zc(i);
     }
     const float wh_zwt = zero;
+    const float s_node = MAXF(th_j / ts_j, 0.01f);
+    const float s1 = MINF(one, s_node);
     FV<1> pK, pS;
     sp.template pick<1>(
         [&](int h) __attribute__((always_inline)) -> FV<1> {
           const int j1 = jwt + 1;
           const float nb = -cs.lay(PF_PSI, j1);
-          bool st = false, sq = false, sw = false;
-          float tq = th_j / ts_j;
-          auto s1of = [&](float t) __attribute__((always_inline)) { return MINF(one, MAXF(t, 0.01f)); };
+          bool sq = false, sw = false;
           float q = divr_d<CS::kRecip>(m, zwtmm, nb, [&]() { return lay_d(cs, PF_RPSI0, j1); }, sq);
           const float e = sel(h, 2.0f * bsw_j + 3.0f, cs.lay(PF_NINVB, j1));
-          float w = m.powf_d(h ? one + q : s1of(tq), e, sw);
-          if (__builtin_expect((h ? sq : st) | sw, 0)) {      // one deferred check
-            divr_fix<CS::kRts>(m, tq, th_j, ts_j);
+          float w = m.powf_d(h ? one + q : s1, e, sw);
+          if (__builtin_expect((h && sq) | sw, 0)) {          // one deferred check
             divr_fix<CS::kRecip>(m, q, zwtmm, nb);
-            w = m.powf(h ? one + q : s1of(tq), e);
+            w = m.powf(h ? one + q : s1, e);
           }
           return FV<1>{{w}};
         },
