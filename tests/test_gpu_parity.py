@@ -118,6 +118,30 @@ def test_gpu_reproduces_bench_stop(kernel, monkeypatch):
     assert same_bits(refcase.pack_state(st, meta["L"]), exp["state_ok"])
 
 
+@pytest.mark.parametrize("kernel", ["pair", "solo"])
+def test_gpu_nan_parameter_cells_match_oracle(kernel, monkeypatch):
+    """Cells with missing soil data (NaN Fmax, a NaN layer parameter) run
+    the year with NaN state, so every deferred special-case check of the
+    substep flags and every redo path runs, in the same waves as normal
+    cells.  A round-2 rewrite of one such path faulted the GPU only on such
+    cells; this covers all of them against the oracle."""
+    monkeypatch.setenv("H9G_KERNEL", kernel)
+    meta, inp, _ = load_golden("c1_10x10")
+    p = {k: v.copy() for k, v in inp["params"].items()}
+    p["fmax"][::7] = np.nan
+    p["psi_s"][3::11, 2] = np.nan
+    p["hksat"][5::13, 0] = np.nan
+    p["bsw"][8::17, 6] = np.nan
+    gpu = h.run(zi=inp["zi"], params=p, forcing=inp["forcing"], nisurf=48, year0=1901, nyears=1,
+                grow_on=True, stop_on_error=False)
+    ref = port.run(zi=inp["zi"], params=p, forcing=inp["forcing"], nisurf=48, year0=1901, nyears=1,
+                   grow_on=1, nthreads=NTHREADS)
+    assert np.isnan(ref["annual"][0]).any(axis=0).sum() > 20
+    assert np.array_equal(gpu["errors"]["code"], ref["errors"]["code"])
+    assert same_bits(gpu["annual"], ref["annual"])
+    assert same_bits(gpu["state"], refcase.pack_state(ref["state"], meta["L"]))
+
+
 def test_reference_stop_raises():
     meta, inp, _ = load_golden("stop_ns24")
     n = meta["ncell"]
