@@ -1200,10 +1200,14 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // independent: one lane of the pair evaluates each.
   float qcharge, sy_first = zero;
   if (jwt < L) {
-    float th_j = zero, ts_j = one, hks_j = zero, bsw_j = zero, smp_m = zero, zq_m = zero, zc_j = zero;
+    // operands of layer jwt+1 (and jwt): the parameters by runtime-indexed
+    // store reads, the register arrays by selects
+    const int j1 = jwt + 1;
+    const float ts_j = cs.lay(PF_TS, j1), hks_j = cs.lay(PF_HKS, j1), bsw_j = cs.lay(PF_BSW, j1);
+    float th_j = zero, smp_m = zero, zq_m = zero, zc_j = zero;
 #pragma unroll
     for (int i = 1; i <= L; i++) {
-      if (i == jwt + 1) { th_j = theta[i]; ts_j = TS(i); hks_j = HKS(i); bsw_j = BSW(i); }
+      if (i == j1) th_j = theta[i];
       if (i == (jwt > 1 ? jwt : 1)) { smp_m = smp[i]; zq_m = zq[i]; }
       if (i == jwt) zc_j = g.zc(i);
     }
