@@ -166,22 +166,29 @@ def cpu_baseline(workload: dict, seed: int) -> dict:
                       f"{'' if ok else ' (a sample process STOPped)'}"}
 
 
-def load_traffic(workload_name: str, kernel: str):
-    """HBM traffic per launch of this kernel, measured with rocprofv3 PMC
-    counters (profiles/pmc_<tag>.json, tools/prof.sh + tools/pmc_summary.py):
-    the latest-tagged summary of the same workload and kernel instantiation."""
+def load_traffic(workload_name: str, kernel: str, build: str | None = None, root: Path = ROOT):
+    """The PMC summary (profiles/pmc_<tag>.json, tools/prof.sh +
+    tools/pmc_summary.py) of this workload and kernel instantiation with the
+    latest tag, and whether it was measured on this build.  Returns
+    (summary, stale_tag): the summary only when its build_id equals `build`
+    (the loaded library's h9g_build_id), else (None, its tag) -- counters of
+    another build are never attached to this run's timing."""
     def norm(k):
         k = k.replace("void ", "").replace("h9k::", "").replace(" ", "")
         return k.split("(")[0]
     best = None
-    for p in sorted((ROOT / "profiles").glob("pmc_*.json")):     # tags sort by round/version
+    for p in sorted((root / "profiles").glob("pmc_*.json")):     # tags sort by round/version
         try:
             d = json.loads(p.read_text())
         except Exception:
             continue
         if d.get("workload") == workload_name and norm(d.get("kernel", "")) == norm(kernel):
             best = d
-    return best
+    if best is None:
+        return None, None
+    if build is None or best.get("build_id") != build:
+        return None, best.get("tag")
+    return best, None
 
 
 def valu_roofline(pmc, launch_s: float):
@@ -326,9 +333,15 @@ def make_exchange(ctx, torch, dist, world: int, device: str):
     device buffer, stream-ordered behind the year kernel with no host
     synchronisation (h9g_get_diagnostics_async), then all-reduced (RCCL
     over xGMI; gloo on CPU in the tests).  Returns (exchange, buffer)."""
-    import hybrid9_amd as h
     if world <= 1:
         return None, None
+    return diag_exchange(ctx, torch, dist, device)
+
+
+def diag_exchange(ctx, torch, dist, device: str):
+    """make_exchange's step for any world size (tests run it at world size 1
+    over RCCL on one GPU)."""
+    import hybrid9_amd as h
     buf = torch.zeros(h.NDIAG, dtype=torch.float64, device=device)
     on_gpu = device.startswith("cuda")
 
@@ -445,7 +458,8 @@ def main():
     launch_s = kern_ms / 1e3 / K
     algo_bytes_launch = cell_steps_rank / K * bytes_per_cell_step(L)
     achieved = algo_bytes_launch / launch_s / 1e9
-    pmc = load_traffic(args.workload, ctx.kernel_name())
+    build = h.build_id()
+    pmc, stale = load_traffic(args.workload, ctx.kernel_name(), build)
     traffic = None
     if pmc and pmc.get("hbm_bytes_per_launch"):
         traffic = pmc["hbm_bytes_per_launch"] / launch_s / 1e9
@@ -477,7 +491,10 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": ctx.kernel_name(), "kernel_ms_per_launch": launch_s * 1e3,
                      "algorithmic_bytes_per_launch": algo_bytes_launch,
-                     "traffic_source": (pmc or {}).get("source"), "valu": valu},
+                     "traffic_source": (pmc or {}).get("source"), "valu": valu,
+                     "build_id": build, "traffic_stale": stale,
+                     "kernel_stats": (pmc or {}).get("kernel_stats"),
+                     "rocprof_ms_per_launch": ((pmc or {}).get("kernel_avg_ns_rocprof") or 0) / 1e6 or None},
         "cpu_baseline": None,
         "diagnostics_last_year": {k: float(v) for k, v in zip(h.DIAG_NAMES, diag)},
         "cells_stopped": failed,

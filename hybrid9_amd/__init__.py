@@ -113,6 +113,7 @@ def lib() -> C.CDLL:
         "h9g_last_kernel_ms": (C.c_float, [vp]),
         "h9g_total_kernel_ms": (C.c_double, [vp, C.c_int]),
         "h9g_kernel_name": (C.c_char_p, [vp]),
+        "h9g_build_id": (C.c_char_p, []),
         "h9g_math_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP]),
         "h9g_div_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP, C.POINTER(C.c_int)]),
         "h9g_math_fast_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP, C.POINTER(C.c_int)]),
@@ -142,6 +143,12 @@ def lib() -> C.CDLL:
         raise H9GError("libh9g ABI mismatch")
     _lib = L
     return L
+
+
+def build_id() -> str:
+    """Digest of the sources and flags the loaded libh9g.so was built from
+    (hybrid9_amd/build.py build_id); needs no GPU."""
+    return lib().h9g_build_id().decode()
 
 
 def exported_symbols():

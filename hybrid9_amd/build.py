@@ -36,6 +36,23 @@ def hipcc() -> str:
     raise FileNotFoundError("hipcc not found")
 
 
+def build_id(extra=()) -> str:
+    """Digest of everything the library is compiled from: the sources, the
+    flags and the target.  It is compiled into the library (h9g_build_id)
+    and recorded with every profile (tools/pmc_summary.py), so bench.py
+    attaches counters only to the build they were measured on."""
+    import hashlib
+    hs = hashlib.sha256()
+    for d in DEPS:
+        hs.update(d.name.encode() + b"\0" + d.read_bytes() + b"\0")
+    hs.update(" ".join([ARCH, *FLAGS, *extra]).encode())
+    return hs.hexdigest()[:16]
+
+
+def id_flag(extra=()) -> str:
+    return f'-DH9G_BUILD_ID="{build_id(extra)}"'
+
+
 def up_to_date() -> bool:
     if not OUT.exists():
         return False
@@ -48,7 +65,8 @@ def build(force: bool = False, verbose: bool = False, extra=()) -> Path:
         return OUT
     OUT.parent.mkdir(parents=True, exist_ok=True)
     tmp = OUT.with_suffix(".so.tmp")
-    cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *extra, str(SRC), str(SRC_IO), "-o", str(tmp)]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *extra, id_flag(extra), str(SRC), str(SRC_IO), "-o",
+           str(tmp)]
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -855,17 +855,25 @@ static int l10_kind(size_t n, int ncu, size_t *n_solo) {
   return t_solo <= t_pair ? 2 : 1;
 }
 
-// Device bytes a context of this configuration allocates (h9g_create and
-// the pair kernel's per-workgroup rollback blocks).
+// Device bytes a context of this configuration allocates: h9g_create's
+// arrays plus what the first h9g_run_year / h9g_soil_layer allocate lazily
+// (the pair kernel's per-workgroup rollback blocks, the pacing rows, the
+// soil build's slow-cell flags).
 size_t h9g_config_bytes(const h9g_config *cfg) {
   if (!cfg || cfg->ncell <= 0 || cfg->nlayers < 1 || cfg->max_days < 1 || cfg->nslots < 1) return 0;
   const size_t n = (size_t)cfg->ncell, L = (size_t)cfg->nlayers;
   const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
   return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * (size_t)cfg->nslots +
                           (12 + L) + 1) * n +
-         sizeof(int) * 5 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
-         ((n + per_block - 1) / per_block) * 65536;
+         sizeof(int) * 6 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
+         ((n + per_block - 1) / per_block) * PairStore<8, H9G_PLANES>::GBLOCK +
+         sizeof(unsigned) * 16 * (size_t)H9G_PACE_ROWS;
 }
+
+// Free HBM h9g_create leaves beyond h9g_config_bytes (HIP runtime, RCCL
+// buffers, allocation granularity), so that a configuration that passes the
+// check at create time does not fail later inside h9g_run_year.
+#define H9G_HEADROOM ((size_t)256 << 20)
 
 static thread_local char g_create_reason[256];
 
@@ -906,10 +914,10 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
   {
     size_t free_b = 0, total_b = 0;
     const size_t need = h9g_config_bytes(cfg);
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && need > free_b) {
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && need + H9G_HEADROOM > free_b) {
       snprintf(g_create_reason, sizeof g_create_reason,
-               "needs %.2f GB of device memory, %.2f GB free (reduce nslots=%d)", need / 1e9, free_b / 1e9,
-               cfg->nslots);
+               "needs %.2f GB of device memory + %.2f GB headroom, %.2f GB free (reduce nslots=%d)", need / 1e9,
+               H9G_HEADROOM / 1e9, free_b / 1e9, cfg->nslots);
       return nullptr;
     }
   }
@@ -1622,6 +1630,13 @@ double h9g_total_kernel_ms(h9g_ctx *ctx, int reset) {
 }
 
 const char *h9g_kernel_name(h9g_ctx *ctx) { return ctx ? ctx->kname : ""; }
+
+#ifndef H9G_BUILD_ID
+#define H9G_BUILD_ID "unknown"
+#endif
+// Digest of the sources and flags this library was compiled from
+// (hybrid9_amd/build.py build_id); profiles record it, bench.py matches it.
+const char *h9g_build_id(void) { return H9G_BUILD_ID; }
 
 int h9g_math_selftest(int device, int n, const float *x, const float *y, float *out) {
   if (n <= 0 || !x || !out) return H9G_EINVAL;

@@ -24,13 +24,14 @@
 // compile-time layer count L, so per-layer values live in registers; the
 // data-dependent index jwt is resolved with unrolled compare/select chains.
 //
-// Speculate-then-verify: the substep is instantiated with a math policy.
-// MathFast runs glibc's main path only (h9m::*_nx, straight-line code) and
-// records whether any input would have taken a special path; the caller
-// then re-runs that substep from the saved state with MathExact (full
-// glibc special-case handling).  Results are therefore bit-identical to
-// MathExact for every input, while the common case carries no per-call
-// branches.
+// Math policies: the substep is instantiated with one.  MathFast runs
+// glibc's main path branch-free (h9m::*_nx) and redoes in place, in a rarely
+// taken branch, any result whose input glibc sends down another path
+// (deferred-check forms *_d / *_fix: one branch per group of independent
+// operations).  MathExact evaluates glibc's full logic and divides.  Results
+// are bit-identical either way.  Only a water-table loop that needs a third
+// layer visit re-runs its substep, exactly, from the rollback copy
+// (h9g_pair.h substep_pair).
 #pragma once
 #include "h9_math.h"
 #include "h9g_geo.h"

@@ -58,6 +58,10 @@ INTERFACE
     IMPORT :: C_PTR
     TYPE(C_PTR) :: h9g_create_error
   END FUNCTION
+  FUNCTION h9g_build_id () BIND(C, NAME='h9g_build_id')
+    IMPORT :: C_PTR
+    TYPE(C_PTR) :: h9g_build_id
+  END FUNCTION
   SUBROUTINE h9g_destroy (ctx) BIND(C, NAME='h9g_destroy')
     IMPORT :: C_PTR
     TYPE(C_PTR), VALUE :: ctx

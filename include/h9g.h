@@ -233,6 +233,10 @@ int h9g_get_params(h9g_ctx *ctx, float *theta_s, float *hksat, float *bsw,
 float h9g_last_kernel_ms(h9g_ctx *ctx);
 double h9g_total_kernel_ms(h9g_ctx *ctx, int reset);
 const char *h9g_kernel_name(h9g_ctx *ctx);
+/* Digest of the sources and compile flags of this library (16 hex digits;
+ * hybrid9_amd/build.py build_id).  Profiles record it, and the bench
+ * attaches counters only to the build they were measured on.  No GPU. */
+const char *h9g_build_id(void);
 
 /* --- self test of the device math (h9_math.h vs glibc) ---------------- */
 /* out[i] = expf(x[i]) if y == NULL, else powf(x[i], y[i]), on device. */

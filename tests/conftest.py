@@ -88,10 +88,19 @@ def load_site_golden(name):
 
 
 def same_bits(a, b):
-    """Bitwise equality with NaN == NaN (any payload) and +0 == -0."""
+    """Bit-for-bit equality of the IEEE bit patterns (+0 and -0 differ: 0 ULP
+    means the same bits), except that any NaN equals any NaN (the payload of
+    a NaN is not a value: the reference marks masked cells NaN)."""
     a = np.asarray(a)
     b = np.asarray(b)
-    return a.shape == b.shape and bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+    if a.shape != b.shape:
+        return False
+    t = np.result_type(a, b)
+    if t.kind != "f":
+        return bool(np.array_equal(a, b))
+    a, b = a.astype(t), b.astype(t)          # f32 -> f64 is exact and keeps the sign of zero
+    u = {2: np.uint16, 4: np.uint32, 8: np.uint64}[t.itemsize]
+    return bool(np.all((a.view(u) == b.view(u)) | (np.isnan(a) & np.isnan(b))))
 
 
 @pytest.fixture(scope="session")

@@ -137,3 +137,71 @@ def test_world2_gloo_bench_exchange():
         assert seed == synth.SEED + rank                 # weak scaling: a grid per rank
         assert n_total == 2 * synth.NLAND05
         assert elapsed >= 0
+
+
+def _pmc(root, tag, build, workload="config2", kernel="void h9g_pair_kernel<8, h9k::GeoC<8, 48> >(KArgs, h9k::GeoC<8, 48>)"):
+    import json
+    (root / "profiles").mkdir(exist_ok=True)
+    (root / "profiles" / f"pmc_{tag}.json").write_text(json.dumps(
+        {"tag": tag, "workload": workload, "kernel": kernel, "build_id": build,
+         "kernel_stats": f"profiles/{tag}_kernel_stats.csv", "hbm_bytes_per_launch": 1e9,
+         "kernel_avg_ns_rocprof": 2e8, "counters_per_launch": {"SQ_INSTS_VALU": 1e11}}))
+
+
+def test_counters_attach_only_to_their_build(tmp_path):
+    """load_traffic attaches the latest summary of the workload and kernel
+    only if it was measured on this build (the r02f line cited
+    the r02e counters)."""
+    k = "h9g_pair_kernel<8,GeoC<8,48>>"
+    assert bench.load_traffic("config2", k, "aaaa", root=tmp_path) == (None, None)
+    _pmc(tmp_path, "r03a", "aaaa")
+    _pmc(tmp_path, "r03b", "bbbb")
+    _pmc(tmp_path, "r03c", "aaaa", workload="config3")
+    pmc, stale = bench.load_traffic("config2", k, "bbbb", root=tmp_path)
+    assert stale is None and pmc["tag"] == "r03b"
+    # the latest config-2 summary is r03b: a library of build aaaa gets no counters
+    assert bench.load_traffic("config2", k, "aaaa", root=tmp_path) == (None, "r03b")
+    assert bench.load_traffic("config2", k, None, root=tmp_path) == (None, "r03b")
+    assert bench.load_traffic("config3", k, "aaaa", root=tmp_path)[0]["tag"] == "r03c"
+    assert bench.load_traffic("config2", "h9g_solo_kernel<8,GeoC<8,48>>", "bbbb", root=tmp_path) == (None, None)
+    assert bench.valu_roofline(None, 0.2) is None
+
+
+def test_build_id_is_the_source_digest():
+    """The loaded library reports the digest of the sources and flags it was
+    built from (a stale .so would report another id)."""
+    from hybrid9_amd import build as hb
+    bid = h.build_id()
+    assert len(bid) == 16 and int(bid, 16) >= 0
+    assert bid == hb.build_id()
+    assert hb.build_id(["-DX"]) != bid
+
+
+def test_pmc_summary_requires_one_build(tmp_path, monkeypatch):
+    """tools/pmc_summary.py refuses a profile whose passes ran different
+    builds, and records the build of one that did not."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("pmc_summary", bench.ROOT / "tools" / "pmc_summary.py")
+    ps = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ps)
+    d = tmp_path / "gpurun_out" / "prof_t1"
+    (d / "kt").mkdir(parents=True)
+    line = lambda b: json.dumps({"metric": "m", "roofline": {"build_id": b}})
+    (d / "kt.log").write_text("x\n" + line("aaaa") + "\n")
+    (d / "sq1.log").write_text(line("bbbb") + "\n")
+    monkeypatch.setattr(ps, "ROOT", tmp_path)
+    with pytest.raises(SystemExit, match="different or unknown builds"):
+        ps.main("t1")
+    (d / "sq1.log").write_text(line("aaaa") + "\n")
+    name = "void h9g_pair_kernel<8, h9k::GeoC<8, 48> >(KArgs, h9k::GeoC<8, 48>)"
+    (d / "kt" / "kt_kernel_stats.csv").write_text(
+        "Name,Calls,TotalDurationNs,AverageNs\n\"%s\",3,600000000,200000000\n" % name)
+    (d / "sq1").mkdir()
+    (d / "sq1" / "x_counter_collection.csv").write_text(
+        "Kernel_Name,Counter_Name,Counter_Value\n\"%s\",SQ_INSTS_VALU,100\n\"%s\",SQ_WAVES,2\n" % (name, name))
+    (tmp_path / "profiles").mkdir()
+    ps.main("t1")
+    out = json.loads((tmp_path / "profiles" / "pmc_t1.json").read_text())
+    assert out["build_id"] == "aaaa" and out["kernel_stats"] == "profiles/t1_kernel_stats.csv"
+    assert out["counters_per_launch"]["SQ_INSTS_VALU"] == 100

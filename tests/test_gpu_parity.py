@@ -1,7 +1,8 @@
 """HIP path (libh9g.so, through the C-ABI) against the reference goldens and
 the CPU oracle.  Bit-for-bit: the north-star tolerance is 1e-6 relative,
-and the implementation is bit-exact, so every comparison here is exact
-(NaN == NaN).  Runs on an MI355X only."""
+and the implementation is bit-exact, so every comparison here compares IEEE
+bit patterns (conftest.same_bits: +0 and -0 differ; any NaN equals any NaN).
+Runs on an MI355X only."""
 import numpy as np
 import pytest
 
@@ -211,9 +212,10 @@ def test_config2_full_grid_sampled_against_oracle():
 def test_config5_l10_quarter_degree_sample(kernel, monkeypatch):
     """10 soil layers (config 5) on 0.25 deg cells, NS=24, GROW on, both
     year kernels and the mixed launch (the L=10 choice follows the column
-    count, h9g.hip l10_kind).  The reference is compiled for 8 layers only
-    (SHARED.f90:294), so L=10 parity is against the oracle restatement
-    (pinned at L=8 by the goldens)."""
+    count, h9g.hip l10_kind), against the C restatement on 2,048 cells.  The
+    restatement is itself pinned at L=10 to the reference's own L=10 build
+    (oracle/_ref/h9ref_l10: SHARED.f90:294,300 set to 10/11) by the golden
+    c5_l10_sample, which test_config5_l10_matches_reference_golden runs here."""
     monkeypatch.setenv("H9G_KERNEL", kernel)
     monkeypatch.setenv("H9G_SPLIT", "1001")
     land = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)
@@ -273,12 +275,16 @@ def test_async_prefetch_pipeline():
     assert same_bits(st, exp["state"])
 
 
-def test_netcdf_prefetch_pipeline(tmp_path):
+@pytest.mark.parametrize("fmt", ["cdf2", "nc4"])
+def test_netcdf_prefetch_pipeline(tmp_path, fmt):
     """READ_PGF path from NetCDF files: the async prefetch (host thread ->
     pinned staging -> copy stream, h9g_nc_forcing_prefetch) of two years of
     PGF-layout files gives the same results as pushing the same forcing
-    directly, and the annual output written as axyYYYY.nc reads back equal."""
+    directly, and the annual output written as axyYYYY.nc reads back equal.
+    Both the classic CDF-2 layout and netCDF-4 (HDF5, chunked + deflate, as
+    PGF v2.1 ships; READ_NET_CDF_3DR.f90:95-97)."""
     from scipy.io import netcdf_file
+    from tests.helpers import write_nc4
     from tests.test_netcdf import write_pgf_like
     nx, ny, nland = 24, 12, 60
     gid, lat = synth.land_cells(nx, ny, nland), None
@@ -288,7 +294,12 @@ def test_netcdf_prefetch_pipeline(tmp_path):
     f = synth.make_forcing(gid, lat, synth.year_day0(1903), nt)          # (7, nt, ncell)
     full = np.full((7, nt, ny * nx), np.float32(250.0))
     full[:, :, gid] = f
-    paths = [write_pgf_like(tmp_path, v, full[k].reshape(nt, ny, nx), 2) for k, v in enumerate(h.PGF_VARS)]
+    if fmt == "nc4":
+        paths = [write_nc4(tmp_path / f"{v}_pgfv2.1_1901-1910.nc4", v, full[k].reshape(nt, ny, nx))
+                 for k, v in enumerate(h.PGF_VARS)]
+        assert open(paths[0], "rb").read(4) == b"\x89HDF"
+    else:
+        paths = [write_pgf_like(tmp_path, v, full[k].reshape(nt, ny, nx), 2) for k, v in enumerate(h.PGF_VARS)]
     d0 = synth.days_in_year(1903)
 
     def run(prefetch):

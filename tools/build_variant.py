@@ -16,7 +16,8 @@ from hybrid9_amd import build as hb  # noqa: E402
 def main() -> None:
     tag, extra = sys.argv[1], sys.argv[2:]
     out = hb.OUT.with_name(f"libh9g_{tag}.so")
-    cmd = [hb.hipcc(), f"--offload-arch={hb.ARCH}", *hb.FLAGS, *extra, str(hb.SRC), str(hb.SRC_IO), "-o", str(out)]
+    cmd = [hb.hipcc(), f"--offload-arch={hb.ARCH}", *hb.FLAGS, *extra, hb.id_flag(extra), str(hb.SRC),
+           str(hb.SRC_IO), "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.exit(f"{tag}: hipcc failed\n{r.stderr[-3000:]}")
