@@ -33,6 +33,9 @@
 #define __forceinline__ inline
 #endif
 
+#ifndef H9G_EXACT_HOOK
+#define H9G_EXACT_HOOK(k0, ns)         // test builds: count the exact re-runs (tests/csrc/host_kernel.cpp)
+#endif
 #if defined(H9G_COUNT_EXACT)
 __device__ unsigned long long h9g_exact_count;   // exact re-runs (lanes), measurement builds only
 __device__ unsigned h9g_exact_wave[1 << 16];     // ... per wave (blockIdx * 4 + wave), pair kernel
@@ -59,11 +62,11 @@ enum : int {
   PS_LAIL, PS_PM, PS_PFM, PS_PLEN, PS_RDEPTH,
   PS_DR0,                              // day-constant reciprocals (kDayRecip): pairs
   PS_DRS = PS_DR0 + 4 * DRP_N,         //   (c.lo s.lo c.hi s.hi), then shared doubles (lo hi)
-  PS_SVZWT = PS_DR0 + 2 * DR_N,        // substep rollback (sv_* of the store)
-  PS_SVWA, PS_SVRNF, PS_SVERR,
+  PS_SVZWT = PS_DR0 + 2 * DR_N,        // day snapshot for the exact re-run (sv_* of the store)
+  PS_SVWA, PS_SVRNF, PS_SVERR, PS_SVNS,
   PS_N
 };
-enum : int { SV_ZWT = 0, SV_WA, SV_RNF, SV_ERR };   // sv_sc fields
+enum : int { SV_ZWT = 0, SV_WA, SV_RNF, SV_ERR, SV_NS };   // sv_sc fields (SV_NS: substep of the snapshot)
 // canopy/soil pairs share a row, canopy in the even column (see D_NUMC)
 static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_DAY + D_DGRAC) % 2 == 0 &&
                   (PS_DAY + D_DRR) % 2 == 0 && (PS_DAY + D_RAC) % 2 == 0 && PS_DR0 % 2 == 0,
@@ -322,7 +325,7 @@ template <int L>
 struct SoloStore {
   static constexpr bool kRecip = false, kRts = false, kDayRecip = false, kRtsHK = false;
   static constexpr int NPF = PF_RPSI0 + 2;           // TS..ROOTR, SVH2O, SVSMP
-  static constexpr int NPS = PS_LAI + 4;             // FMAX..DAY, SV*
+  static constexpr int NPS = PS_LAI + 5;             // FMAX..DAY, SV*
   static constexpr int ROWS = NPF * L + NPS;
   lds_float *b;
   const lds_float *zt;
@@ -849,14 +852,19 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           const float temp0 = m.powf_d(b0, expo, s0);
           const float tpi = m.powf_d(bi, expo, si);
           bad |= s0 | si;
-          // water table inside the layer (:530-543)
+          // water table inside the layer (:530-543): at most one layer of a
+          // column, so evaluated only in a slot where some lane of the wave
+          // has it (a wave-uniform branch)
+          float vin = zero;
+          if (any_lane(inl)) {
           const float d0 = zwtmm - zlo;
           const float q1 = m.div_d(OWN(PF_PTE), d0, recip64(d0));
           const float voleq1 = q1 * (one - temp0);
-          float vin = m.div_d(voleq1 * (zwtmm - zlo) + ts * (zhi - zwtmm), zhi - zlo, cs.rdz_t(il));
+          vin = m.div_d(voleq1 * (zwtmm - zlo) + ts * (zhi - zwtmm), zhi - zlo, cs.rdz_t(il));
           bad |= inl && (m.div_bad(q1) | m.div_bad(vin));
           vin = MINF(ts, vin);
           vin = MAXF(vin, zero);
+          }
           // water table below the layer (:548-558)
           float vbl = OWN(PF_C3) * (tpi - temp0);
           vbl = MAXF(vbl, 0.0f);
@@ -874,7 +882,14 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   //   lane 0: temp0 of the aquifer node (:579-580), then zq(L+1) (:581-590);
   //   lane 1: the specific-yield power of layer L (:937-940), then smp1 of
   //           the aquifer row (:737-741).
-  FV<1> pA, pY;
+  // The aquifer node's powers and row (:574-590, :737-741, :937-940) are read
+  // only by lanes whose water table is below the column: a wave with none
+  // skips them (wave-uniform); the deepening loop's rare fall-through below
+  // the column then evaluates s_y(L) itself.
+  const bool any_aq = any_lane(aq);
+  FV<1> pA{{one}}, pY{{one}};
+  FV<2> eA{{zero, zero}}, eS{{zero, zero}};
+  if (any_aq) {
   sp.template pick<1>(
       [&](int h) __attribute__((always_inline)) -> FV<1> {
         const float npsi = -PSI(L);
@@ -884,7 +899,6 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
         return FV<1>{{m.powf(sel(h, q, one + q), sel(h, one + ninv, ninv))}};
       },
       pA, pY);
-  FV<2> eA, eS;
   {
     const float d0 = aq ? (zwtmm - g.zi(L)) : one;
     float ve = LAYF(PF_PTE, L) / d0 * (1.0f - pA.v[0]);
@@ -892,17 +906,32 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     ve = MINF(TS(L), ve);
     sp.template pick<2>(
         [&](int h) __attribute__((always_inline)) -> FV<2> {
-          const float q2 = divr<CS::kRts>(m, sel(h, ve, theta[L]), TS(L), [&]() { return lay_d(cs, PF_RTS0, L); });
-          float sn = MAXF(0.5f * (one + q2), 0.01f);
-          sn = MINF(one, sn);
-          float x = sel(h, MAXF(q2, 0.01f), sn);
-          if (!aq) x = one;
-          float z = PSI(L) * m.powf(x, -BSW(L));
+          // the quotient's and the power's checks deferred to one branch
+          // (round 2's d878d3e, backed out after a GPU fault that the calls
+          // of the then out-of-line redo caused: DESIGN.md §3)
+          const float xn = sel(h, ve, theta[L]);
+          auto xof = [&](float q2) __attribute__((always_inline)) {
+            float sn = MAXF(0.5f * (one + q2), 0.01f);
+            sn = MINF(one, sn);
+            const float x = sel(h, MAXF(q2, 0.01f), sn);
+            return aq ? x : one;
+          };
+          bool sq = false, sw = false;
+          float q2 = divr_d<CS::kRts>(m, xn, TS(L), [&]() { return lay_d(cs, PF_RTS0, L); }, sq);
+          float x = xof(q2);
+          float pw = m.powf_d(x, -BSW(L), sw);
+          if (__builtin_expect(sq | sw, 0)) {
+            divr_fix<CS::kRts>(m, q2, xn, TS(L));
+            x = xof(q2);
+            pw = m.powf(x, -BSW(L));
+          }
+          float z = PSI(L) * pw;
           z = MAXF(smpmin, z);
           return FV<2>{{z, -BSW(L) * z / (x * TS(L))}};
         },
         eA, eS);
   }
+  }  // any_aq
   zq[L + 1] = aq ? eA.v[0] : zero;
   const float smp1 = eS.v[0], dsmpdw1 = eS.v[1];
   cs.launder();
@@ -1041,7 +1070,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     for (int i = 1; i <= L - 1; i++)
       flux3_f(hk[i], (smp[i + 1] - smp[i]) - (zq[i + 1] - zq[i]), dsmpdw[i], dsmpdw[i + 1], dhkdw[i], g.den(i),
               g.rden(i), i, bad);
-    {                                  // aquifer interface (used when aq)
+    qo[L] = d1[L] = d2[L] = zero;
+    if (any_aq) {                      // aquifer interface (used when aq)
       const float den = zcA - g.zc(L);
       bool ba = false;
       flux3_f(hk[L], smp1 - smp[L] - (zq[L + 1] - zq[L]), dsmpdw[L], dsmpdw1, dhkdw[L], den, recip64(den), L, ba);
@@ -1278,7 +1308,10 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
         s.zwt = cs.zim(i);
         return i != L;
       });
-      if (qcharge_tot > zero) s.zwt = s.zwt - m.div(qcharge_tot, 1000.0f, r1000) / rous;
+      if (qcharge_tot > zero) {
+        if (!any_aq) rous = s_y_at(L, zwtmm);    // pY was skipped: the same expression
+        s.zwt = s.zwt - m.div(qcharge_tot, 1000.0f, r1000) / rous;
+      }
     }
     jwt2 = jwt_of<L>(s.zwt, zim);
   }
@@ -1429,10 +1462,29 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
 #undef OWN
 }
 
-// Exact re-run of a substep from the rollback area (rare path, out of line):
-// one lane computes every layer with the full glibc special-case logic.
+// The day snapshot (sv_* of the store): the state at the start of substep
+// SV_NS of the current day -- h2osoi_liq, smp, zwt, wa and the runoff sum.
+// cell_year_pair writes it once a day (SV_NS = 0); the exact re-run below
+// advances it.  Round 2 rewrote it before every substep (11 stores per lane
+// per substep, 4.5 GB per config-2 launch written back from L2) although
+// only the rare re-run reads it.
+template <int L, class SP, class CS>
+H9K_HD void save_day(const SP &sp, const CS &cs, const St<L> &s, float rnf_sum) {
+  save_layers<L>(sp, cs, 0, s.h2o);
+  save_layers<L>(sp, cs, 1, s.smp);
+  cs.sv_set_sc(SV_ZWT, s.zwt);
+  cs.sv_set_sc(SV_WA, s.wa);
+  cs.sv_set_sc(SV_RNF, rnf_sum);
+  cs.sv_set_sc(SV_NS, zero);
+}
+
+// Exact re-run (rare path, out of line): from the snapshot (the state at
+// the start of substep SV_NS of the day) through substep ns, one lane
+// computing every layer with the full glibc special-case logic.  The fast
+// path's substeps before ns are bit-identical to these, so replaying them
+// reproduces its state exactly.  The snapshot then holds the state after ns.
 template <int L, class G, class CS>
-H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const double *l2) {
+H9K_RARE int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const double *l2, int ns) {
   cs.sv_sync();
   St<L> s;
 #pragma unroll
@@ -1446,7 +1498,10 @@ H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const dou
   MathExact me{{e2, l2}};
   const SplitAll sa;
   NoProf np;
-  const int code = hydrology_pair<L, G, MathExact, SplitAll, CS>(*g, cs, sa, s, rnf, errval, me, np);
+  int code = 0;
+  H9G_EXACT_HOOK((int)cs.sv_sc(SV_NS), ns);
+  for (int k = (int)cs.sv_sc(SV_NS); k <= ns && !code; k++)
+    code = hydrology_pair<L, G, MathExact, SplitAll, CS>(*g, cs, sa, s, rnf, errval, me, np);
   cs.launder();
 #pragma unroll
   for (int i = 1; i <= L; i++) {
@@ -1457,30 +1512,31 @@ H9K_COLD int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const dou
   cs.sv_set_sc(SV_WA, s.wa);
   cs.sv_set_sc(SV_RNF, rnf);
   cs.sv_set_sc(SV_ERR, errval);
+  cs.sv_set_sc(SV_NS, (float)(ns + 1));
   cs.sv_sync();
   return code;
 }
 
-// One substep, speculate-then-verify (as substep in h9g_step.h).  A pair
-// re-runs if either of its lanes saw a special-path input.
+// Substep ns of the day on the fast path.  A pair re-runs (exactly, from the
+// day snapshot) if either of its lanes needs a third water-table layer visit.
 template <int L, class G, class SP, class CS, class PR>
 H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_sum, float &errval,
-                        const h9m::Tabs &T, PR &pr) {
+                        const h9m::Tabs &T, PR &pr, int ns) {
   pr.mark(0);
-  save_layers<L>(sp, cs, 0, s.h2o);
-  save_layers<L>(sp, cs, 1, s.smp);
-  cs.sv_set_sc(SV_ZWT, s.zwt);
-  cs.sv_set_sc(SV_WA, s.wa);
-  cs.sv_set_sc(SV_RNF, rnf_sum);
   MathFast mf{T, false};
   int code = hydrology_pair<L, G, MathFast, SP, CS, PR>(g, cs, sp, s, rnf_sum, errval, mf, pr);
+#if defined(H9G_FORCE_RERUN)
+  // test builds: also re-run every H9G_FORCE_RERUN-th substep of a day (the
+  // exact replay from the day snapshot must reproduce the fast path's state)
+  if (ns % H9G_FORCE_RERUN == H9G_FORCE_RERUN - 1) mf.special = true;
+#endif
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
 #if defined(H9G_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)
     atomicAdd(&h9g_exact_count, 1ull);      // measurement builds only
     atomicAdd(&h9g_exact_wave[(blockIdx.x * 4 + (threadIdx.x >> 6)) & 0xffff], 1u);
 #endif
     cs.launder();
-    code = substep_exact_pair<L, G, CS>(&g, cs, T.exp2, T.log2);
+    code = substep_exact_pair<L, G, CS>(&g, cs, T.exp2, T.log2, ns);
     cs.launder();
 #pragma unroll
     for (int i = 1; i <= L; i++) {
@@ -1539,8 +1595,9 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
       else
         day_consts(d, s.LAI, s.LAI_litter, cs, me);
     }
+    save_day<L>(sp, cs, s, rnf_sum);
     for (int ns = 0; ns < nisurf; ns++) {                            // :193-211
-      code = substep_pair<L, G, SP, CS>(g, cs, sp, s, rnf_sum, errval, T, pr);
+      code = substep_pair<L, G, SP, CS>(g, cs, sp, s, rnf_sum, errval, T, pr, ns);
       if (code) { eday = day; estep = ns; break; }
     }
     cs.launder();

@@ -144,17 +144,20 @@ struct MathExact {
   H9K_HD bool div_bad(float) const { return false; }
   H9K_HD void div_fix(float &, float, float) {}
 };
-// Out-of-line, cold: the exact re-run of a substep (h9g_pair.h).
+// The rare paths -- glibc's special cases of MathFast below and the exact
+// re-run of a substep (h9g_pair.h) -- are inlined into the kernels, which
+// make no calls.  Round 2 kept them out of line; the kernels' calls were
+// miscompiled: a lane-mask SGPR stayed live across calls to the redo
+// function, which overwrites it (tools/isa_calls.py).
 #if defined(__HIP_DEVICE_COMPILE__)
-#define H9K_COLD __device__ __attribute__((noinline, cold))
+#define H9K_RARE __device__ __forceinline__
 #else
-#define H9K_COLD static __attribute__((noinline, cold))
+#define H9K_RARE static __attribute__((noinline, cold))
 #endif
 
-// glibc's full expf / powf, out of line: the in-place redo of MathFast
-// (rare), kept out of the hot loop's code and register allocation.
-H9K_COLD float expf_redo(float x, const uint64_t *e2, const double *l2) { return h9m::expf(x, {e2, l2}); }
-H9K_COLD float powf_redo(float x, float y, const uint64_t *e2, const double *l2) {
+// glibc's full expf / powf: the in-place redo of MathFast (rare).
+H9K_RARE float expf_redo(float x, const uint64_t *e2, const double *l2) { return h9m::expf(x, {e2, l2}); }
+H9K_RARE float powf_redo(float x, float y, const uint64_t *e2, const double *l2) {
   return h9m::powf(x, y, {e2, l2});
 }
 

@@ -7,6 +7,15 @@
 // a GPU.  Never linked into the product library.
 #include <stdint.h>
 #include <string.h>
+// exact re-runs: count, runs replaying from a snapshot taken before substep
+// 0 of a later substep (several substeps replayed), substeps replayed
+static long long g_exact[3];
+#define H9G_EXACT_HOOK(k0, ns)                      \
+  do {                                              \
+    __atomic_add_fetch(&g_exact[0], 1, __ATOMIC_RELAXED); \
+    if ((ns) > (k0)) __atomic_add_fetch(&g_exact[1], 1, __ATOMIC_RELAXED); \
+    __atomic_add_fetch(&g_exact[2], (ns) - (k0) + 1, __ATOMIC_RELAXED); \
+  } while (0)
 #include "../../hybrid9_amd/csrc/h9g_geo.h"
 #include "../../hybrid9_amd/csrc/h9g_step.h"
 #include "../../hybrid9_amd/csrc/h9g_pair.h"
@@ -150,4 +159,9 @@ extern "C" int h9k_host_site(int n, int L, int nisurf, int nday, int use_const_g
   if (cg && nisurf == 48) RS(10, (GeoC<10, 48>()));
   RS(10, make_geo_r<10>(zi, nisurf));
 #undef RS
+}
+
+// Exact re-run counters since the last call (then reset).
+extern "C" void h9k_host_exact_stats(long long *out) {
+  for (int i = 0; i < 3; i++) out[i] = __atomic_exchange_n(&g_exact[i], 0, __ATOMIC_RELAXED);
 }

@@ -55,3 +55,18 @@ def test_no_cpu_fallback_without_gpu():
         assert "h9g_create failed" in str(e)
     else:
         raise AssertionError("Context created without a GPU")
+
+
+def test_device_code_makes_no_calls():
+    """Every kernel of libh9g.so is call-free: the rare paths (glibc's special
+    cases, the exact re-run) are inlined.  Calls from the kernels were
+    miscompiled in round 2 -- a lane-mask SGPR stayed live across calls of the
+    out-of-line redo function, which overwrites it (DESIGN.md §3,
+    tools/isa_calls.py)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("isa_calls", Path(__file__).resolve().parents[1] / "tools" / "isa_calls.py")
+    ic = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ic)
+    calls = ic.calls_per_function(h.LIB_PATH)
+    assert any("h9g_pair_kernel" in k for k in calls)
+    assert {k: n for k, n in calls.items() if n} == {}

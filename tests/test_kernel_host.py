@@ -18,6 +18,18 @@ from tests.helpers import BUILD, ROOT
 _lib = None
 
 
+def _build_lib(extra):
+    src = ROOT / "tests" / "csrc" / "host_kernel.cpp"
+    out = BUILD / ("libhost_kernel%s.so" % ("_" + "_".join(f.strip("-D").lower().replace("=", "")
+                                                          for f in extra) if extra else ""))
+    deps = [src] + list((ROOT / "hybrid9_amd" / "csrc").glob("*.h"))
+    if not out.exists() or out.stat().st_mtime < max(d.stat().st_mtime for d in deps):
+        BUILD.mkdir(exist_ok=True)
+        subprocess.run(["g++", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fopenmp",
+                        "-std=c++17", "-fPIC", "-shared", *extra, str(src), "-o", str(out)], check=True)
+    return out
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -35,7 +47,7 @@ def lib():
     return _lib
 
 
-def host_run(*, zi, params, forcing, nisurf, year0, nyears, grow_on, state0, const_geo):
+def host_run(*, zi, params, forcing, nisurf, year0, nyears, grow_on, state0, const_geo, so=None):
     L = params["theta_s"].shape[1]
     n = params["fmax"].size
     zi = np.ascontiguousarray(zi, np.float32)
@@ -45,7 +57,7 @@ def host_run(*, zi, params, forcing, nisurf, year0, nyears, grow_on, state0, con
     ann = np.zeros((nyears, 12 + L, n), np.float32)
     err = np.zeros(4 * n, np.int32)
     fp = C.POINTER(C.c_float)
-    rc = lib().h9k_host_run(n, L, nisurf, int(grow_on), year0, nyears, int(const_geo),
+    rc = (so or lib()).h9k_host_run(n, L, nisurf, int(grow_on), year0, nyears, int(const_geo),
                             zi.ctypes.data_as(fp), pp.ctypes.data_as(fp), fo.ctypes.data_as(fp),
                             st.ctypes.data_as(fp), ann.ctypes.data_as(fp),
                             err.ctypes.data_as(C.POINTER(C.c_int)))
@@ -107,3 +119,24 @@ def test_kernel_body_degenerate_exponents():
     assert ref["rc"] == out["rc"]
     assert same_bits(out["annual"], ref["annual"])
     assert same_bits(out["state"], refcase.pack_state(ref["state"], 8))
+
+
+@pytest.mark.parametrize("name", ["edge", "c1_2yr_leap", "c4_spinup"])
+def test_exact_rerun_replays_from_day_snapshot(name):
+    """The exact re-run (a third water-table layer visit) replays from the
+    day snapshot (h9g_pair.h save_day / substep_exact_pair) through its
+    substep.  A test build forces a re-run at every 5th substep of a day, so
+    each replays several substeps, and also re-runs right after a re-run of
+    the same day; the result must still be the reference's bit for bit."""
+    so = C.CDLL(str(_build_lib(["-DH9G_FORCE_RERUN=5"])))
+    so.h9k_host_run.argtypes = lib().h9k_host_run.argtypes
+    meta, inp, exp = load_golden(name)
+    st = np.zeros(3, np.int64)
+    so.h9k_host_exact_stats(st.ctypes.data_as(C.POINTER(C.c_longlong)))   # reset
+    out = host_run(const_geo=1, so=so, **inp)
+    so.h9k_host_exact_stats(st.ctypes.data_as(C.POINTER(C.c_longlong)))
+    assert out["rc"] == 0
+    assert same_bits(out["annual"], exp["annual"]) and same_bits(out["state"], exp["state"])
+    runs, multi, replayed = st
+    ncell, days = meta["ncell"], int(inp["forcing"].shape[1])
+    assert runs >= ncell * days * (inp["nisurf"] // 5) and multi > 0 and replayed > 4 * runs, st
