@@ -83,6 +83,19 @@ struct KArgs {
   int prio_mode;                   // Pacer mode: 0 none, 1 rotate, 2 pace
 };
 
+// XCD-aware workgroup order.  MI355X deals the workgroups of a launch
+// round-robin to its 8 XCDs (workgroup b -> XCD b % 8), each with its own L2.
+// Workgroup b works on the cells of virtual workgroup xcd_vwg(b), which makes
+// each XCD's workgroups one contiguous range of cells: the forcing, annual
+// sums and state lines an XCD touches are its own (no line fetched by two
+// XCDs), and the per-year cell sort (h9g_sort_kernel) reorders cells only
+// within an XCD's range.
+#define H9G_NXCD 8
+__host__ __device__ __forceinline__ unsigned xcd_vwg(unsigned b, unsigned nb) {
+  const unsigned x = b % H9G_NXCD, q = nb / H9G_NXCD, r = nb % H9G_NXCD;
+  return x * q + (x < r ? x : r) + b / H9G_NXCD;
+}
+
 __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
   const int t = threadIdx.x;
   if (t < 32) {
@@ -98,7 +111,7 @@ __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
 // Waves per SIMD: 3 at L = 8 (168 VGPRs, 3 x 53 KB LDS per CU); 2 at L = 10,
 // where 168 VGPRs spill ~90 registers into the substep loop.
 template <int L>
-constexpr int pair_waves() { return L <= 8 ? 3 : 2; }
+constexpr int pair_waves() { return pair_resident<L>(); }
 
 template <int L, class G>
 __global__ void __launch_bounds__(64 * H9G_PWAVES)
@@ -115,7 +128,7 @@ h9g_pair_kernel(const KArgs a, const G g) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane >= H9G_PLANES) return;
   const int h = lane & 1;
-  const int slot = a.c0 + (blockIdx.x * H9G_PWAVES + wave) * H9G_PCPW + (lane >> 1);
+  const int slot = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * H9G_PCPW + (lane >> 1);
   if (slot >= a.cend) return;        // both lanes of a pair leave together
   const int c = a.perm ? a.perm[slot] : slot;
   const int n = a.ncell;
@@ -220,7 +233,7 @@ h9g_solo_kernel(const KArgs a, const G g) {
   if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};
-  const int slot = a.c0 + blockIdx.x * blockDim.x + threadIdx.x;
+  const int slot = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x);
   if (slot >= a.cend) return;
   const int c = a.perm ? a.perm[slot] : slot;
   const int n = a.ncell;
@@ -298,17 +311,25 @@ h9g_solo_kernel(const KArgs a, const G g) {
 // changes no result; it makes the 22 columns of a wave take the same
 // jwt-dependent branches (equilibrium-profile cases :517-567, recharge
 // :856-904, water-table and drainage loops :923-1118), which otherwise
-// diverge once water tables rise into the columns.  One block.
+// diverge once water tables rise into the columns.  Block x sorts the slots
+// of XCD x's workgroups of the year launch over [c0, cend) with cpb cells per
+// workgroup (xcd_vwg), so no cell leaves its XCD's range.
 template <int L, class G>
-__global__ void __launch_bounds__(1024) h9g_sort_kernel(int n, const float *__restrict__ st,
+__global__ void __launch_bounds__(1024) h9g_sort_kernel(int n, int c0, int cend, int cpb, const float *__restrict__ st,
                                                         const int *__restrict__ err, int *__restrict__ perm,
                                                         const G g) {
   constexpr int NK = L + 2;
   __shared__ int cnt[NK][1024];
   __shared__ int base[NK];
   const int t = threadIdx.x;
-  const int per = (n + 1023) / 1024;
-  const int b = t * per, e = min(n, b + per);
+  const unsigned nb = (unsigned)((cend - c0 + cpb - 1) / cpb), x = blockIdx.x;
+  const unsigned q = nb / H9G_NXCD, r = nb % H9G_NXCD;
+  const int p0 = c0 + (int)(x * q + (x < r ? x : r)) * cpb;
+  const int p1 = min(cend, p0 + (int)(q + (x < r ? 1u : 0u)) * cpb);
+  const int m = p1 - p0;
+  if (m <= 0) return;                      // (uniform per block)
+  const int per = (m + 1023) / 1024;
+  const int b = p0 + t * per, e = min(p1, b + per);
   float zim[L + 1];
 #pragma unroll
   for (int i = 1; i <= L; i++) zim[i] = g.zim(i);
@@ -352,7 +373,7 @@ __global__ void __launch_bounds__(1024) h9g_sort_kernel(int n, const float *__re
 #pragma unroll
     for (int j = 0; j < NK; j++)
       if (j == k) pos = loc[j]++;
-    perm[pos] = c;
+    perm[p0 + pos] = c;
   }
 }
 
@@ -832,21 +853,21 @@ void h9g_destroy(h9g_ctx *ctx) {
 
 // Kernel for L = 10 (1: pair, 2: solo, 3: both).  They are bit-identical
 // and differ in how n columns quantise into rounds of resident waves.  The
-// solo kernel (1-wave blocks, 1 wave/SIMD: 256 VGPRs + 100 AGPRs) packs 64
-// columns per wave; the pair kernel (88-column blocks, 2 waves/SIMD by LDS)
-// 22.  Time per round measured on config 5 (270,000 columns, 1 GPU): solo
-// 693 ms / 5, pair 725 ms / 6.  Kind 3 runs the whole solo rounds and hands
-// the remainder (less than one solo round) to the pair kernel: at 0.25 deg
-// on one GPU that is 4 solo rounds + 1 pair round instead of 5 solo rounds.
-// Smaller strong-scaling shards take the pair kernel.  Returns the kind and
-// sets *n_solo (cells [0, n_solo) on the solo kernel, for kind 3).
+// solo kernel (1-wave blocks, 1 wave/SIMD: its 36.6 KB LDS column store
+// allows four per CU) packs 64 columns per wave; the pair kernel
+// (88-column blocks, 3 waves/SIMD, pair_resident) 22.  Time per round
+// measured on config 5 (270,000 columns, 1 GPU, round 3): solo 659 ms / 5,
+// pair 535 ms / 4.  Kind 3 runs the whole solo rounds and hands the
+// remainder (less than one solo round) to the pair kernel.  Returns the kind
+// and sets *n_solo (cells [0, n_solo) on the solo kernel, for kind 3).
 static int l10_kind(size_t n, int ncu, size_t *n_solo) {
   const size_t per_pair = (size_t)H9G_PCPW * H9G_PWAVES, solo_round = (size_t)4 * ncu * H9G_YBLOCK;
-  auto pair_rounds = [&](size_t m) { return ((m + per_pair - 1) / per_pair + 2 * (size_t)ncu - 1) / (2 * (size_t)ncu); };
+  const size_t pair_slots = (size_t)pair_resident<10>() * ncu;
+  auto pair_rounds = [&](size_t m) { return ((m + per_pair - 1) / per_pair + pair_slots - 1) / pair_slots; };
   const size_t rs = (n + solo_round - 1) / solo_round;
-  const size_t t_solo = rs * 1386, t_pair = pair_rounds(n) * 1208;
+  const size_t t_solo = rs * 1318, t_pair = pair_rounds(n) * 1338;
   const size_t full = n / solo_round;
-  const size_t t_mixed = full * 1386 + pair_rounds(n - full * solo_round) * 1208;
+  const size_t t_mixed = full * 1318 + pair_rounds(n - full * solo_round) * 1338;
   *n_solo = 0;
   if (full >= 1 && n > full * solo_round && t_mixed < t_solo && t_mixed < t_pair) {
     *n_solo = full * solo_round;
@@ -1160,7 +1181,7 @@ static int pace_mode(const h9g_ctx *ctx, size_t m) {
   if (ctx->prio_mode >= 0) return ctx->prio_mode;
   const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
   const size_t blocks = (m + per_block - 1) / per_block;
-  return blocks <= (size_t)ctx->ncu * (ctx->L <= 8 ? 3 : 2) ? 2 : 1;
+  return blocks <= (size_t)ctx->ncu * (ctx->L <= 8 ? pair_resident<8>() : pair_resident<10>()) ? 2 : 1;
 }
 
 int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
@@ -1188,8 +1209,19 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   a.stamps = nullptr;
   a.sv = nullptr;
   a.perm = nullptr;
-  if (ctx->sort) {
-    H9G_DISPATCH(ctx, h9g_sort_kernel, 1, 1024, ctx->sc, (int)ctx->n, ctx->d_st, ctx->d_err, ctx->d_perm);
+  if (ctx->sort) {             // per launch range and its workgroup size (h9g_sort_kernel)
+    const int n = (int)ctx->n, ns = (int)ctx->n_solo, pcpb = H9G_PCPW * H9G_PWAVES;
+    if (ctx->kind == 2) {
+      H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, 1024, ctx->sc, n, 0, n, H9G_YBLOCK, ctx->d_st, ctx->d_err, ctx->d_perm);
+    } else if (ctx->kind == 3) {
+      if (ns > 0)
+        H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, 1024, ctx->sc, n, 0, ns, H9G_YBLOCK, ctx->d_st, ctx->d_err,
+                     ctx->d_perm);
+      if (ns < n)
+        H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, 1024, ctx->sc, n, ns, n, pcpb, ctx->d_st, ctx->d_err, ctx->d_perm);
+    } else {
+      H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, 1024, ctx->sc, n, 0, n, pcpb, ctx->d_st, ctx->d_err, ctx->d_perm);
+    }
     HIPCHK(hipGetLastError());
     a.perm = ctx->d_perm;
   }

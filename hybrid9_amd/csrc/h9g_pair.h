@@ -230,23 +230,30 @@ __device__ __forceinline__ void pace_key(int &row, int &slot) {
 #endif
 }
 
+// The L = 10 pair kernel runs 3 waves per SIMD like L = 8: without the
+// per-layer double reciprocals of -psi and theta_s its LDS block fits three
+// workgroups per CU (48.6 KB), and 168 VGPRs (config 5: 632 -> 535 ms per
+// year against 2 waves/SIMD with the reciprocals).
+template <int L>
+constexpr int pair_resident() { return 3; }   // waves per SIMD (h9g.hip pair_waves)
+
 template <int L, int S>
 struct PairStore {
   static constexpr int NT = L / 2;
-  static constexpr bool kRecip = true, kRts = true, kDayRecip = true;
+  static constexpr bool kRecip = L <= 8, kRts = kRecip, kDayRecip = true;
 #if defined(H9G_RTSHK)
   static constexpr bool kRtsHK = true;
 #else
-  static constexpr bool kRtsHK = L > 8;                     // 256-VGPR kernels (h9g.hip pair_waves)
+  static constexpr bool kRtsHK = kRts && pair_resident<L>() == 2;   // 256-VGPR kernels (h9g.hip pair_waves)
 #endif
-  static constexpr int NPF = kRts ? PF_SVH2O : PF_RTS0;     // per-layer fields in LDS
+  static constexpr int NPF = kRecip ? (kRts ? PF_SVH2O : PF_RTS0) : PF_RPSI0;   // per-layer fields in LDS
   static constexpr int NPS = kDayRecip ? PS_SVZWT : PS_DR0; // per-cell fields in LDS
   static constexpr int ROWS = NPF * NT + (NPS + 1) / 2;
   static constexpr int GBLOCK = 65536;                      // bytes per workgroup (>= any LDS address)
   lds_float *self, *even;
   const lds_float *zt;                 // zi(0..L+1), then zi(0..L+1)/1000 (per block)
   float *svw;                          // this workgroup's rollback block (global)
-  static constexpr int RESIDENT = L <= 8 ? 3 : 2;          // workgroups per CU = waves per SIMD (h9g.hip pair_waves)
+  static constexpr int RESIDENT = pair_resident<L>();       // workgroups per CU = waves per SIMD (h9g.hip pair_waves)
   Pacer pace;
   __device__ __forceinline__ void day_start(int day) const { pace.day_start(day, RESIDENT); }
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
@@ -697,7 +704,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
 #pragma unroll
     for (int i = 1; i <= L; i++) {
       float b = one - qb[i];
-      b = MINF(one, b);
+      b = MINC(one, b);
       b = MAXF(zero, b);
       beta = beta + ROOT(i) * b;
     }
@@ -828,8 +835,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
             }
           }
           const float qv = divr<CS::kRts>(m, vol_eq, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); });
-          float z = psi * m.powf(MAXF(qv, 0.01f), -OWN(PF_BSW));
-          return FV<1>{{MAXF(smpmin, z)}};
+          float z = psi * m.powf(MAXX(qv, 0.01f), -OWN(PF_BSW));
+          return FV<1>{{MAXC(smpmin, z)}};
     };
     // fast: the same values branch-free (all three cases evaluated, the
     // layer's selected); bad = some quotient or power of the selected case
@@ -842,10 +849,10 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           const bool sat = zwtmm <= zlo;
           const bool inl = (zwtmm < zhi) && (zwtmm > zlo);
           const float expo = one + OWN(PF_NINVB);
-          const double rp = join_d(OWN(PF_RPSI0), OWN(PF_RPSI1));
+          auto rp = [&]() __attribute__((always_inline)) { return join_d(OWN(PF_RPSI0), OWN(PF_RPSI1)); };
           const float n0 = ((-psi) + zwtmm - zlo), ni = (-psi + zwtmm - zhi);
-          float b0 = divr_d<CS::kRecip>(m, n0, -psi, [&]() { return rp; }, bad);
-          float bi = divr_d<CS::kRecip>(m, ni, -psi, [&]() { return rp; }, bad);
+          float b0 = divr_d<CS::kRecip>(m, n0, -psi, rp, bad);
+          float bi = divr_d<CS::kRecip>(m, ni, -psi, rp, bad);
           b0 = sat ? one : b0;
           bi = (sat || inl) ? one : bi;
           bool s0, si;
@@ -872,9 +879,9 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           const float vol_eq = sat ? ts : (inl ? vin : vbl);
           const float qv = divr_d<CS::kRts>(m, vol_eq, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }, bad);
           bool sz;
-          const float z = psi * m.powf_d(MAXF(qv, 0.01f), -OWN(PF_BSW), sz);
+          const float z = psi * m.powf_d(MAXX(qv, 0.01f), -OWN(PF_BSW), sz);
           bad |= sz;
-          return FV<1>{{MAXF(smpmin, z)}};
+          return FV<1>{{MAXC(smpmin, z)}};
     };
     sp.template par_d<NT, 1, H9G_FE_EQ>(eq_fast, eq_exact, out);
   }
@@ -911,9 +918,9 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           // of the then out-of-line redo caused: DESIGN.md §3)
           const float xn = sel(h, ve, theta[L]);
           auto xof = [&](float q2) __attribute__((always_inline)) {
-            float sn = MAXF(0.5f * (one + q2), 0.01f);
-            sn = MINF(one, sn);
-            const float x = sel(h, MAXF(q2, 0.01f), sn);
+            float sn = MAXX(0.5f * (one + q2), 0.01f);
+            sn = MINC(one, sn);
+            const float x = sel(h, MAXX(q2, 0.01f), sn);
             return aq ? x : one;
           };
           bool sq = false, sw = false;
@@ -926,7 +933,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
             pw = m.powf(x, -BSW(L));
           }
           float z = PSI(L) * pw;
-          z = MAXF(smpmin, z);
+          z = MAXC(smpmin, z);
           return FV<2>{{z, -BSW(L) * z / (x * TS(L))}};
         },
         eA, eS);
@@ -949,13 +956,13 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           const float ts = OWN(PF_TS);
           const float tsp = sel(h, TS(i0 + 1), TS(ip1));
           float s1 = 0.5f * (th + thp) / (0.5f * (ts + tsp));
-          s1 = MINF(one, s1);
+          s1 = MINC(one, s1);
           const float bsw = OWN(PF_BSW);
           // (s_node from the reciprocal only with room to spare in VGPRs: +35
           // spilled VGPRs at 168, measured)
-          float s_node = MAXF(divr<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }),
+          float s_node = MAXX(divr<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }),
                               0.01f);
-          s_node = MINF(one, s_node);
+          s_node = MINC(one, s_node);
           // the two powers are independent: one deferred check
           const float ek = 2.0f * bsw + 2.0f, es = -bsw;
           bool sk, ss;
@@ -970,7 +977,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           r.v[0] = s1 * s2;
           r.v[1] = (2.0f * bsw + 3.0f) * s2 * OWN(PF_ITS);
           float sm = OWN(PF_PSI) * ps;
-          sm = MAXF(smpmin, sm);
+          sm = MAXC(smpmin, sm);
           r.v[2] = sm;
           r.v[3] = (-bsw) * sm / (s_node * ts);
           return r;
@@ -984,11 +991,11 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           const float ts = OWN(PF_TS);
           const float tsp = sel(h, TS(i0 + 1), TS(ip1));
           float s1 = 0.5f * (th + thp) / (0.5f * (ts + tsp));
-          s1 = MINF(one, s1);
+          s1 = MINC(one, s1);
           const float bsw = OWN(PF_BSW);
-          float s_node = MAXF(divr_d<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }, bad),
+          float s_node = MAXX(divr_d<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }, bad),
                               0.01f);
-          s_node = MINF(one, s_node);
+          s_node = MINC(one, s_node);
           const float ek = 2.0f * bsw + 2.0f, es = -bsw;
           bool sk, ss;
           const float pk = m.powf_d(s1, ek, sk);
@@ -999,7 +1006,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           r.v[0] = s1 * s2;
           r.v[1] = (2.0f * bsw + 3.0f) * s2 * OWN(PF_ITS);
           float sm = OWN(PF_PSI) * ps;
-          sm = MAXF(smpmin, sm);
+          sm = MAXC(smpmin, sm);
           r.v[2] = sm;
           r.v[3] = (-bsw) * sm / (s_node * ts);
           return r;
@@ -1219,7 +1226,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     return one + divr<CS::kRecip>(m, zmm, -cs.lay(PF_PSI, i), [&]() { return lay_d(cs, PF_RPSI0, i); });
   };
   auto s_y_of = [&](int i, float pw) __attribute__((always_inline)) -> float {
-    return MAXF(cs.lay(PF_TS, i) * (one - pw), 0.02f);
+    return MAXX(cs.lay(PF_TS, i) * (one - pw), 0.02f);
   };
   auto s_y_at = [&](int i, float zmm) __attribute__((always_inline)) -> float {
     return s_y_of(i, m.powf(s_y_base(i, zmm), cs.lay(PF_NINVB, i)));
@@ -1242,8 +1249,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
       if (i == jwt) zc_j = g.zc(i);
     }
     const float wh_zwt = zero;
-    const float s_node = MAXF(th_j / ts_j, 0.01f);
-    const float s1 = MINF(one, s_node);
+    const float s_node = MAXX(th_j / ts_j, 0.01f);
+    const float s1 = MINC(one, s_node);
     FV<1> pK, pS;
     sp.template pick<1>(
         [&](int h) __attribute__((always_inline)) -> FV<1> {
@@ -1262,14 +1269,14 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
         pK, pS);
     sy_first = s_y_of(jwt + 1, pS.v[0]);
     const float ka = hks_j * pK.v[0];
-    const float smp1m = MAXF(smpmin, smp_m);
+    const float smp1m = MAXC(smpmin, smp_m);
     const float wh = smp1m - zq_m;
     if (jwt == 0)
       qcharge = -ka * (wh_zwt - wh) / (zwtmm + one);
     else
       qcharge = -ka * (wh_zwt - wh) / ((zwtmm - zc_j) * 2.0f);
-    qcharge = MAXF(-10.0f / dt, qcharge);
-    qcharge = MINF(10.0f / dt, qcharge);
+    qcharge = MAXC(-10.0f / dt, qcharge);
+    qcharge = MINC(10.0f / dt, qcharge);
   } else {
     qcharge = m.div(dwat2[L + 1] * dzA, dt, g.rdt());
   }
@@ -1277,7 +1284,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // the layers the loops visit (usually one), at a runtime layer index (the
   // first visit's from the pick above); rous = s_y(L) of the pre-update
   // zwtmm came from the pair split of the equilibrium profile.
-  float rous = MAXF(TS(L) * (one - pY.v[0]), 0.02f);
+  float rous = MAXX(TS(L) * (one - pY.v[0]), 0.02f);
   int jwt2 = jwt;
   if (jwt == L) {
     s.wa = s.wa + qcharge * dt;
@@ -1379,7 +1386,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   }
   // :1122-1123
   s.zwt = MAXF(0.0f, s.zwt);
-  s.zwt = MINF(80.0f, s.zwt);
+  s.zwt = MINC(80.0f, s.zwt);
   cs.launder();
   pr.mark(6);
   // :1131-1137 saturation excess, bottom-up bucket
@@ -1464,18 +1471,19 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
 
 // The day snapshot (sv_* of the store): the state at the start of substep
 // SV_NS of the current day -- h2osoi_liq, smp, zwt, wa and the runoff sum.
-// cell_year_pair writes it once a day (SV_NS = 0); the exact re-run below
+// cell_year_pair writes it at most once a day, before the day's first
+// substep with the water table in the column; the exact re-run below
 // advances it.  Round 2 rewrote it before every substep (11 stores per lane
 // per substep, 4.5 GB per config-2 launch written back from L2) although
 // only the rare re-run reads it.
 template <int L, class SP, class CS>
-H9K_HD void save_day(const SP &sp, const CS &cs, const St<L> &s, float rnf_sum) {
+H9K_HD void save_day(const SP &sp, const CS &cs, const St<L> &s, float rnf_sum, int ns) {
   save_layers<L>(sp, cs, 0, s.h2o);
   save_layers<L>(sp, cs, 1, s.smp);
   cs.sv_set_sc(SV_ZWT, s.zwt);
   cs.sv_set_sc(SV_WA, s.wa);
   cs.sv_set_sc(SV_RNF, rnf_sum);
-  cs.sv_set_sc(SV_NS, zero);
+  cs.sv_set_sc(SV_NS, (float)ns);
 }
 
 // Exact re-run (rare path, out of line): from the snapshot (the state at
@@ -1524,11 +1532,15 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
                         const h9m::Tabs &T, PR &pr, int ns) {
   pr.mark(0);
   MathFast mf{T, false};
+#if defined(H9G_FORCE_RERUN)
+  const bool in_column = s.zwt <= g.zim(L);   // the substeps that may re-run (cell_year_pair)
+#endif
   int code = hydrology_pair<L, G, MathFast, SP, CS, PR>(g, cs, sp, s, rnf_sum, errval, mf, pr);
 #if defined(H9G_FORCE_RERUN)
-  // test builds: also re-run every H9G_FORCE_RERUN-th substep of a day (the
-  // exact replay from the day snapshot must reproduce the fast path's state)
-  if (ns % H9G_FORCE_RERUN == H9G_FORCE_RERUN - 1) mf.special = true;
+  // test builds: also re-run every H9G_FORCE_RERUN-th substep of a day that
+  // could (the exact replay from the day snapshot must reproduce the fast
+  // path's state)
+  if (in_column && ns % H9G_FORCE_RERUN == H9G_FORCE_RERUN - 1) mf.special = true;
 #endif
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
 #if defined(H9G_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)
@@ -1588,15 +1600,34 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
     const gbl_float *f = forc + (size_t)day * fday;
     opaque(f);
     {
-      const Day d = make_day(f[0 * fvar], f[1 * fvar], f[2 * fvar], f[3 * fvar], f[4 * fvar],
-                             f[5 * fvar], f[6 * fvar]);                // :168-184
+      float fv[7];             // tas rlds rsds huss ps pr rhs
+#pragma unroll
+      for (int k = 0; k < 7; k++) fv[k] = ld_stream(f + k * fvar);
+      const Day d = make_day(fv[0], fv[1], fv[2], fv[3], fv[4], fv[5], fv[6]);   // :168-184
       if constexpr (Park)
         day_consts(d, cs.sc(PS_LAI), cs.sc(PS_LAIL), cs, me);
       else
         day_consts(d, s.LAI, s.LAI_litter, cs, me);
+      // :235-241, the forcing's running sums: they depend on the forcing
+      // only, so they are added here, once the day's forcing is loaded, and
+      // the forcing is read once a day (the reference adds them after the
+      // substeps: the same values in the same order; a cell that STOPs has
+      // NaN annual means either way)
+      float a7[7];
+#pragma unroll
+      for (int k = 0; k < 7; k++) a7[k] = A[(A_TAS + k) * as];
+#pragma unroll
+      for (int k = 0; k < 7; k++) A[(A_TAS + k) * as] = a7[k] + fv[k];
     }
-    save_day<L>(sp, cs, s, rnf_sum);
+    bool snapped = false;
     for (int ns = 0; ns < nisurf; ns++) {                            // :193-211
+      // the day snapshot, taken before the first substep of the day whose
+      // water table is in the column (jwt < L): only such a substep visits
+      // layers (:923-1118), so only it can need the exact re-run
+      if (!snapped && s.zwt <= g.zim(L)) {
+        save_day<L>(sp, cs, s, rnf_sum, ns);
+        snapped = true;
+      }
       code = substep_pair<L, G, SP, CS>(g, cs, sp, s, rnf_sum, errval, T, pr, ns);
       if (code) { eday = day; estep = ns; break; }
     }
@@ -1611,27 +1642,19 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
     }
     if (code) return code;
     opaque(A);
-    opaque(f);                 // re-read the day's forcing (not kept live over the substeps)
-    const float tas = f[0 * fvar], rlds = f[1 * fvar], rsds = f[2 * fvar], huss = f[3 * fvar];
-    const float ps = f[4 * fvar], pr = f[5 * fvar], rhs = f[6 * fvar];
     if (grow_on) {
-      grow_day<L, G, MathExact>(g, tas, s, cs, npp, me);              // :217
+      opaque(f);               // tas again (not kept live over the substeps)
+      grow_day<L, G, MathExact>(g, ld_stream(f), s, cs, npp, me);       // :217
       park();
     }
-    // :235-254.  All running sums are loaded before any is stored, so the
+    // :242-254.  All running sums are loaded before any is stored, so the
     // loads issue back to back (the compiler cannot prove the strided
     // fields distinct)
+    auto later = [](int k) { return k != A_RNF && k != A_EVAP && (k < A_TAS || k > A_RHS); };
     float a[12 + L];
 #pragma unroll
     for (int k = 0; k < 12 + L; k++)
-      if (k != A_RNF && k != A_EVAP) a[k] = A[k * as];
-    a[A_TAS] = a[A_TAS] + tas;
-    a[A_RLDS] = a[A_RLDS] + rlds;
-    a[A_RSDS] = a[A_RSDS] + rsds;
-    a[A_HUSS] = a[A_HUSS] + huss;
-    a[A_PS] = a[A_PS] + ps;
-    a[A_PR] = a[A_PR] + pr;
-    a[A_RHS] = a[A_RHS] + rhs;
+      if (later(k)) a[k] = A[k * as];
     a[A_PM] = a[A_PM] + s.pm;
     a[A_NPP] = a[A_NPP] + npp;
     float h2o_sum = a[A_H2O];
@@ -1644,7 +1667,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
     a[A_H2O] = h2o_sum;
 #pragma unroll
     for (int k = 0; k < 12 + L; k++)
-      if (k != A_RNF && k != A_EVAP) A[k * as] = a[k];
+      if (later(k)) A[k * as] = a[k];
   }
   // :263-290
   opaque(A);

@@ -59,6 +59,35 @@ H9K_HD float MAXF(float a, float b) { return a > b ? a : b; }
 H9K_HD float MINF(float a, float b) { return a < b ? a : b; }
 #endif
 H9K_HD float absf(float a) { return __builtin_fabsf(a); }
+// MIN/MAX with a NONZERO constant c, one VALU instead of compare + select:
+//   MAXC(c, x) = flang's MAX(c, x) = c > x ? c : x.  For x NaN that is x, for
+//     x == c it is x (the same bits, as c is not a zero): exactly IEEE
+//     754-2019 maximum(c, x) (NaN-propagating; v_maximum3_f32 on gfx950);
+//   MAXX(x, c) = MAX(x, c) = x > c ? x : c: c for x NaN, i.e. maxNum(x, c)
+//     (v_max_f32).
+// With c = 0 they would differ in the sign of a zero result, so zeros keep
+// MAXF/MINF.  (A NaN's payload may differ; no result but a NaN depends on it.)
+H9K_HD float MAXC(float c, float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_elementwise_maximum(c, x);
+#else
+  return MAXF(c, x);
+#endif
+}
+H9K_HD float MINC(float c, float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_elementwise_minimum(c, x);
+#else
+  return MINF(c, x);
+#endif
+}
+H9K_HD float MAXX(float x, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fmaxf(x, c);
+#else
+  return MAXF(x, c);
+#endif
+}
 
 // Scheduling fence: stops the machine scheduler from interleaving the
 // unrolled per-layer bodies (each a few powf with double-precision
@@ -266,6 +295,18 @@ typedef __attribute__((address_space(1))) float gbl_float;
 typedef float lds_float;
 typedef float gbl_float;
 #endif
+
+// Loads of the forcing slab, which streams through L2 once per cell-day:
+// with the non-temporal hint, so that it does not evict the L2-resident
+// annual sums and day snapshots (config 2: HBM writes 4.9 -> 3.2 GB per
+// launch; with the XCD-aware cell order 0.6 GB).
+H9K_HD float ld_stream(const gbl_float *p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 
 template <int L>
 struct St {            // persistent per-cell state (SHARED.f90), in registers

