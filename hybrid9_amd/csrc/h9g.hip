@@ -78,6 +78,7 @@ struct KArgs {
   unsigned *__restrict__ stamps;   // H9G_STAMPS builds: 8 phase cycle sums per wave
   float *__restrict__ sv;          // pair kernel: substep rollback, PairStore::GBLOCK bytes per workgroup
   const int *__restrict__ perm;    // lane slot -> cell (h9g_sort_kernel), or null: identity
+  int *__restrict__ hist;          // per cell: substeps of the year with the water table below the column
   unsigned *__restrict__ pace;     // pair kernel, Pacer mode 2: H9G_PACE_ROWS x 16 progress words
   unsigned epoch;                  // Pacer mode 2: launch tag
   int prio_mode;                   // Pacer mode: 0 none, 1 rotate, 2 pace
@@ -192,6 +193,7 @@ h9g_pair_kernel(const KArgs a, const G g) {
   int cw = c;
   opaque(cw);
   cs.launder();
+  if (a.hist) a.hist[cw] = s.naq;
   const size_t ow = (size_t)(4 * L + 1) * n + cw;
 #pragma unroll
   for (int i = 1; i <= L; i++) {
@@ -278,6 +280,7 @@ h9g_solo_kernel(const KArgs a, const G g) {
   int cw = c;
   opaque(cw);
   cs.launder();
+  if (a.hist) a.hist[cw] = s.naq;
   const size_t ow = (size_t)(4 * L + 1) * n + cw;
 #pragma unroll
   for (int i = 1; i <= L; i++) {
@@ -306,20 +309,32 @@ h9g_solo_kernel(const KArgs a, const G g) {
 }
 
 // Cell order of the next year kernel: a stable counting sort of the cells
-// by the layer holding their water table (jwt, HYDROLOGY.f90:499-508, from
-// the current zwt), failed cells last.  Cells are independent, so the order
-// changes no result; it makes the 22 columns of a wave take the same
-// jwt-dependent branches (equilibrium-profile cases :517-567, recharge
-// :856-904, water-table and drainage loops :923-1118), which otherwise
-// diverge once water tables rise into the columns.  Block x sorts the slots
-// of XCD x's workgroups of the year launch over [c0, cend) with cpb cells per
-// workgroup (xcd_vwg), so no cell leaves its XCD's range.
+// by where their water table was over the last year, failed cells last.
+// Cells are independent, so the order changes no result; it makes the 22
+// columns of a wave take the same branches that depend on the layer holding
+// the water table (jwt, HYDROLOGY.f90:499-508): the equilibrium-profile cases
+// (:517-567), the aquifer node (:574-590, :737-741) for jwt = L, the recharge
+// (:856-904) and the water-table and drainage loops (:923-1118) for jwt < L.
+// A wave holding both kinds of column runs both.  Keys:
+//   0 .. L-1   no substep of the last year below the column: the current jwt
+//   L .. L+7   some: the fraction of the year's substeps below it, in eighths
+//   L+8        every substep below the column
+//   L+9        failed
+// Without a last year (hist < 0) the current jwt decides (jwt = L: key L+8).
+// Round 2 sorted by the current jwt alone; cells whose water table crosses
+// the column's bottom during the year then sat in waves of both kinds
+// (measured with H9G_COUNT_BRANCH at 1906-1907: 84% of the wave-substeps ran
+// the aquifer node, 81% the recharge).  Block x sorts the slots of XCD x's
+// workgroups of the year launch over [c0, cend) with cpb cells per workgroup
+// (xcd_vwg), so no cell leaves its XCD's range.
+#define H9G_SORT_THREADS 512
 template <int L, class G>
-__global__ void __launch_bounds__(1024) h9g_sort_kernel(int n, int c0, int cend, int cpb, const float *__restrict__ st,
-                                                        const int *__restrict__ err, int *__restrict__ perm,
-                                                        const G g) {
-  constexpr int NK = L + 2;
-  __shared__ int cnt[NK][1024];
+__global__ void __launch_bounds__(H9G_SORT_THREADS)
+    h9g_sort_kernel(int n, int c0, int cend, int cpb, const float *__restrict__ st, const int *__restrict__ err,
+                    const int *__restrict__ hist, int nsub, int *__restrict__ perm, const G g) {
+  constexpr int NK = L + 10;
+  constexpr int NTH = H9G_SORT_THREADS;
+  __shared__ int cnt[NK][NTH];
   __shared__ int base[NK];
   const int t = threadIdx.x;
   const unsigned nb = (unsigned)((cend - c0 + cpb - 1) / cpb), x = blockIdx.x;
@@ -328,13 +343,21 @@ __global__ void __launch_bounds__(1024) h9g_sort_kernel(int n, int c0, int cend,
   const int p1 = min(cend, p0 + (int)(q + (x < r ? 1u : 0u)) * cpb);
   const int m = p1 - p0;
   if (m <= 0) return;                      // (uniform per block)
-  const int per = (m + 1023) / 1024;
+  const int per = (m + NTH - 1) / NTH;
   const int b = p0 + t * per, e = min(p1, b + per);
   float zim[L + 1];
 #pragma unroll
   for (int i = 1; i <= L; i++) zim[i] = g.zim(i);
   const float *zwt = st + (size_t)(4 * L + 1) * n;
-  auto key = [&](int c) -> int { return err[c] ? L + 1 : jwt_of<L>(zwt[c], zim); };
+  auto key = [&](int c) -> int {
+    if (err[c]) return L + 9;
+    const int j = jwt_of<L>(zwt[c], zim);
+    const int h = hist ? hist[c] : -1;
+    if (h < 0 || nsub <= 0) return j < L ? j : L + 8;
+    if (h == 0) return j < L ? j : L;
+    if (h >= nsub) return L + 8;
+    return L + (int)((long long)h * 8 / nsub);
+  };
   int loc[NK];
 #pragma unroll
   for (int k = 0; k < NK; k++) loc[k] = 0;
@@ -348,7 +371,7 @@ __global__ void __launch_bounds__(1024) h9g_sort_kernel(int n, int c0, int cend,
   __syncthreads();
   if (t < NK) {                   // exclusive scan of each key's counts over the threads
     int sum = 0;
-    for (int j = 0; j < 1024; j++) {
+    for (int j = 0; j < NTH; j++) {
       const int v = cnt[t][j];
       cnt[t][j] = sum;
       sum += v;
@@ -739,6 +762,8 @@ struct h9g_ctx {
   int *d_slow = nullptr;
   float *d_sv = nullptr;          // pair kernel rollback blocks
   int *d_perm = nullptr;          // cell order of the year kernel (h9g_sort_kernel)
+  int *d_hist = nullptr;          // per cell: substeps of the last year below the column (-1: none)
+  int hist_nsub = 0;              // substeps of that year
   unsigned *d_pace = nullptr;     // Pacer mode 2 progress rows (h9g_pair.h)
   unsigned epoch = 0;
   int prio_mode = -1;             // H9G_PRIO: 0 none, 1 rotate, 2 pace; -1 auto (pace_mode)
@@ -802,6 +827,10 @@ static GeoKind geo_kind(const h9g_config &c) {
     }                                                                                \
   } while (0)
 
+#if defined(H9G_ISA_ONLY)
+// tools/isa_pair.sh: device code of the config-2 pair kernel alone (ISA study)
+template __global__ void h9g_pair_kernel<8, GeoC<8, 48>>(const KArgs, const GeoC<8, 48>);
+#else
 static unsigned nblocks(size_t n) { return (unsigned)((n + H9G_BLOCK - 1) / H9G_BLOCK); }
 
 extern "C" {
@@ -836,6 +865,7 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_stamps);
   (void)hipFree(ctx->d_slow);
   (void)hipFree(ctx->d_perm);
+  (void)hipFree(ctx->d_hist);
   (void)hipFree(ctx->d_pace);
   for (auto e : ctx->ev_copied) hipEventDestroy(e);
   for (auto e : ctx->ev_consumed) hipEventDestroy(e);
@@ -886,7 +916,7 @@ size_t h9g_config_bytes(const h9g_config *cfg) {
   const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
   return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * (size_t)cfg->nslots +
                           (12 + L) + 1) * n +
-         sizeof(int) * 6 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
+         sizeof(int) * 7 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
          ((n + per_block - 1) / per_block) * PairStore<8, H9G_PLANES>::GBLOCK +
          sizeof(unsigned) * 16 * (size_t)H9G_PACE_ROWS;
 }
@@ -960,12 +990,14 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
             hipMalloc(&ctx->d_diag, sizeof(double) * H9G_NDIAG) == hipSuccess &&
             hipMalloc(&ctx->d_gid, sizeof(int64_t) * n) == hipSuccess &&
             hipMalloc(&ctx->d_lat, sizeof(float) * n) == hipSuccess &&
-            hipMalloc(&ctx->d_perm, sizeof(int) * n) == hipSuccess;
+            hipMalloc(&ctx->d_perm, sizeof(int) * n) == hipSuccess &&
+            hipMalloc(&ctx->d_hist, sizeof(int) * n) == hipSuccess;
   if (ok) {
     ok = hipMemset(ctx->d_err, 0, sizeof(int) * 4 * n) == hipSuccess &&
          hipMemset(ctx->d_errflag, 0, sizeof(int)) == hipSuccess &&
          hipMemset(ctx->d_diag, 0, sizeof(double) * H9G_NDIAG) == hipSuccess &&
-         hipMemset(ctx->d_ann, 0xff, sizeof(float) * (12 + L) * n) == hipSuccess;
+         hipMemset(ctx->d_ann, 0xff, sizeof(float) * (12 + L) * n) == hipSuccess &&
+         hipMemset(ctx->d_hist, 0xff, sizeof(int) * n) == hipSuccess;
   }
   ctx->slot_days.assign(cfg->nslots, 0);
   ctx->h_pin.assign(cfg->nslots, nullptr);
@@ -1074,6 +1106,8 @@ int h9g_init_state(h9g_ctx *ctx) {
   HIPCHK(hipMemsetAsync(ctx->d_err, 0, sizeof(int) * 4 * ctx->n, ctx->sc));
   HIPCHK(hipMemsetAsync(ctx->d_errflag, 0, sizeof(int), ctx->sc));
   HIPCHK(hipStreamSynchronize(ctx->sc));
+  HIPCHK(hipMemsetAsync(ctx->d_hist, 0xff, sizeof(int) * ctx->n, ctx->sc));   // a new state has no last year
+  ctx->hist_nsub = 0;
   ctx->state_set = 1;
   ctx->last_err = h9g_error{};
   return 0;
@@ -1103,6 +1137,8 @@ int h9g_set_state(h9g_ctx *ctx, const float *packed) {
   HIPCHK(hipMemsetAsync(ctx->d_err, 0, sizeof(int) * 4 * n, ctx->sc));
   HIPCHK(hipMemsetAsync(ctx->d_errflag, 0, sizeof(int), ctx->sc));
   HIPCHK(hipStreamSynchronize(ctx->sc));
+  HIPCHK(hipMemsetAsync(ctx->d_hist, 0xff, sizeof(int) * ctx->n, ctx->sc));   // a new state has no last year
+  ctx->hist_nsub = 0;
   ctx->state_set = 1;
   ctx->last_err = h9g_error{};
   return 0;
@@ -1209,18 +1245,22 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   a.stamps = nullptr;
   a.sv = nullptr;
   a.perm = nullptr;
+  a.hist = ctx->d_hist;
   if (ctx->sort) {             // per launch range and its workgroup size (h9g_sort_kernel)
     const int n = (int)ctx->n, ns = (int)ctx->n_solo, pcpb = H9G_PCPW * H9G_PWAVES;
     if (ctx->kind == 2) {
-      H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, 1024, ctx->sc, n, 0, n, H9G_YBLOCK, ctx->d_st, ctx->d_err, ctx->d_perm);
+      H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, n, H9G_YBLOCK, ctx->d_st, ctx->d_err,
+                   ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
     } else if (ctx->kind == 3) {
       if (ns > 0)
-        H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, 1024, ctx->sc, n, 0, ns, H9G_YBLOCK, ctx->d_st, ctx->d_err,
-                     ctx->d_perm);
+        H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, ns, H9G_YBLOCK, ctx->d_st,
+                     ctx->d_err, ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
       if (ns < n)
-        H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, 1024, ctx->sc, n, ns, n, pcpb, ctx->d_st, ctx->d_err, ctx->d_perm);
+        H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, ns, n, pcpb, ctx->d_st, ctx->d_err,
+                     ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
     } else {
-      H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, 1024, ctx->sc, n, 0, n, pcpb, ctx->d_st, ctx->d_err, ctx->d_perm);
+      H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, n, pcpb, ctx->d_st, ctx->d_err,
+                   ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
     }
     HIPCHK(hipGetLastError());
     a.perm = ctx->d_perm;
@@ -1292,6 +1332,7 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)ctx->n, ctx->L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
   HIPCHK(hipGetLastError());
   ctx->last_year = jyear;
+  ctx->hist_nsub = nt * ctx->cfg.nisurf;
   ctx->ran = 1;
   return 0;
 }
@@ -1380,6 +1421,23 @@ int h9g_sync(h9g_ctx *ctx) {
     fprintf(stderr, "h9g exact re-runs: %zu waves;", top.size());
     for (size_t k = 0; k < top.size() && k < 8; k++) fprintf(stderr, " w%d:%u", top[k].second, top[k].first);
     fprintf(stderr, "\n");
+  }
+#endif
+#if defined(H9G_COUNT_BRANCH)
+  {  // waves entering each H9G_BR site per wave-substep since the last sync, and their mean active lanes
+    static const char *names[BR_N] = {"substep", "theta", "qb", "eq_exact", "aqpow", "aq_s", "hk_exact", "tri_flux",
+                                      "tri_sweep", "recharge", "baseflow", "watmin", "rerun", "powf_redo",
+                                      "div_redo", "expf_redo", "powf_fix", "div_fix", "inl", "any_aq", "jwt_col",
+                                      "visit2", "snap", "day"};
+    unsigned long long c[64];
+    HIPCHK(hipMemcpyFromSymbol(c, HIP_SYMBOL(h9g_branch_count), sizeof(c)));
+    const double ws = c[BR_SUBSTEP] ? (double)c[BR_SUBSTEP] : 1.0;
+    fprintf(stderr, "h9g branch counts (wave entries per wave-substep, mean lanes):");
+    for (int k = 0; k < BR_N; k++)
+      if (c[k]) fprintf(stderr, " %s=%.4g/%.1f", names[k], c[k] / ws, (double)c[32 + k] / c[k]);
+    fprintf(stderr, "\n");
+    memset(c, 0, sizeof(c));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(h9g_branch_count), c, sizeof(c)));
   }
 #endif
   int flag = 0;
@@ -1801,3 +1859,4 @@ float h9g_host_powf(float x, float y) {
 }
 
 }  // extern "C"
+#endif  // H9G_ISA_ONLY

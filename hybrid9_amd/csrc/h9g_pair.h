@@ -97,6 +97,19 @@ H9K_HD float pair_swap(float v) {
 #endif
 }
 
+// value of the pair's even (E = 0) or odd (E = 1) lane, in both lanes (DPP
+// quad_perm [0,0,2,2] / [1,1,3,3]): one instruction instead of pair_swap
+// plus a select per lane
+template <int E>
+H9K_HD float pair_bcast(float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int x = __builtin_bit_cast(int, v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(x, E ? 0xF5 : 0xA0, 0xF, 0xF, true));
+#else
+  return v;
+#endif
+}
+
 // A double kept as two float fields (low word, high word).
 H9K_HD double join_d(float lo, float hi) {
   return __builtin_bit_cast(double, (uint64_t)__builtin_bit_cast(uint32_t, hi) << 32 |
@@ -241,11 +254,9 @@ template <int L, int S>
 struct PairStore {
   static constexpr int NT = L / 2;
   static constexpr bool kRecip = L <= 8, kRts = kRecip, kDayRecip = true;
-#if defined(H9G_RTSHK)
-  static constexpr bool kRtsHK = true;
-#else
-  static constexpr bool kRtsHK = kRts && pair_resident<L>() == 2;   // 256-VGPR kernels (h9g.hip pair_waves)
-#endif
+  // s_node of the conductivity phase from the stored 1/theta_s too (round 3:
+  // no longer spills in the call-free kernel)
+  static constexpr bool kRtsHK = kRts;
   static constexpr int NPF = kRecip ? (kRts ? PF_SVH2O : PF_RTS0) : PF_RPSI0;   // per-layer fields in LDS
   static constexpr int NPS = kDayRecip ? PS_SVZWT : PS_DR0; // per-cell fields in LDS
   static constexpr int ROWS = NPF * NT + (NPS + 1) / 2;
@@ -456,6 +467,13 @@ struct SplitAll {
 // Two lanes per column (device fast path); h = lane & 1.
 struct Split2 {
   int h;
+  // v of the even lane -> e, of the odd lane -> o, in both lanes: two DPP
+  // broadcasts (round 3; round 2 swapped and selected per lane: one DPP
+  // move and two selects, 214.5 -> 213.9 ms)
+  H9K_HD void xchg(float v, float &e, float &o) const {
+    e = pair_bcast<0>(v);
+    o = pair_bcast<1>(v);
+  }
   template <class CS>
   H9K_HD float own(const CS &cs, int p, int t, int) const { return cs.slot(p, t); }
   // FE: a scheduling fence after every FE slots (FE > 1 lets the scheduler
@@ -466,11 +484,7 @@ struct Split2 {
     for (int t = 0; t < NT; t++) {
       const FV<K> r = f(t, h);
 #pragma unroll
-      for (int k = 0; k < K; k++) {
-        const float o = pair_swap(r.v[k]);
-        out[k][2 * t + 1] = sel(h, r.v[k], o);
-        out[k][2 * t + 2] = sel(h, o, r.v[k]);
-      }
+      for (int k = 0; k < K; k++) xchg(r.v[k], out[k][2 * t + 1], out[k][2 * t + 2]);
       if ((t + 1) % FE == 0 || t == NT - 1) sched_fence();
     }
   }
@@ -494,22 +508,14 @@ struct Split2 {
 #pragma unroll
     for (int t = 0; t < NT; t++) {
 #pragma unroll
-      for (int k = 0; k < K; k++) {
-        const float o = pair_swap(r[t].v[k]);
-        out[k][2 * t + 1] = sel(h, r[t].v[k], o);
-        out[k][2 * t + 2] = sel(h, o, r[t].v[k]);
-      }
+      for (int k = 0; k < K; k++) xchg(r[t].v[k], out[k][2 * t + 1], out[k][2 * t + 2]);
     }
   }
   template <int K, class F>
   H9K_HD void pick(F f, FV<K> &r0, FV<K> &r1) const {
     const FV<K> r = f(h);
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-      const float o = pair_swap(r.v[k]);
-      r0.v[k] = sel(h, r.v[k], o);
-      r1.v[k] = sel(h, o, r.v[k]);
-    }
+    for (int k = 0; k < K; k++) xchg(r.v[k], r0.v[k], r1.v[k]);
   }
   H9K_HD bool pair_any(bool p) const {
     const float f = p ? 1.0f : 0.0f;
@@ -591,6 +597,7 @@ H9K_HD void visit_layers(M &m, F visit) {
   } else {
     bool more = visit(0);
     if (any_lane(more)) {
+      H9G_BR(BR_VISIT2);
       if (more) more = visit(1);
       m.special |= more;
     }
@@ -677,6 +684,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     bad |= m.div_bad(theta[i]);
   }
   if (__builtin_expect(bad, 0)) {
+    H9G_BR(BR_THETA);
 #pragma unroll
     for (int i = 1; i <= L; i++) m.div_fix(theta[i], h2o[i], g.thk(i));
   }
@@ -698,6 +706,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
       badb |= m.div_bad(qb[i]);
     }
     if (__builtin_expect(badb, 0)) {
+      H9G_BR(BR_QB);
 #pragma unroll
       for (int i = 1; i <= L; i++) m.div_fix(qb[i], smp[i] - g.zc(i), -150000.0f);
     }
@@ -782,12 +791,16 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   cs.launder();
   pr.mark(1);
 
-  // :517-567 equilibrium profile, own layers
+  // :517-567 equilibrium profile and :598-639 conductivity and matric
+  // potential, own layers (independent phases)
   float zq[L + 2];
+  float hk[L + 1], dhkdw[L + 1], dsmpdw[L + 1];
   {
-    float *const out[1] = {zq};
+    float *const outq[1] = {zq};
+    float *const outk[4] = {hk, dhkdw, smp, dsmpdw};
     // exact: the reference expression with every special case redone in place
     auto eq_exact = [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
+          H9G_BR(BR_EQX);
           const int i0 = 2 * t + 1;                           // own layer il = i0 + h
           const int il = i0 + h;
           const float zlo = cs.zi(il - 1), zhi = cs.zi(il);   // zi(i-1), zi(i): geometry table
@@ -864,6 +877,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           // has it (a wave-uniform branch)
           float vin = zero;
           if (any_lane(inl)) {
+          H9G_BR(BR_INL);
           const float d0 = zwtmm - zlo;
           const float q1 = m.div_d(OWN(PF_PTE), d0, recip64(d0));
           const float voleq1 = q1 * (one - temp0);
@@ -883,72 +897,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           bad |= sz;
           return FV<1>{{MAXC(smpmin, z)}};
     };
-    sp.template par_d<NT, 1, H9G_FE_EQ>(eq_fast, eq_exact, out);
-  }
-  // Four single powers split over the pair (unused ones get base 1):
-  //   lane 0: temp0 of the aquifer node (:579-580), then zq(L+1) (:581-590);
-  //   lane 1: the specific-yield power of layer L (:937-940), then smp1 of
-  //           the aquifer row (:737-741).
-  // The aquifer node's powers and row (:574-590, :737-741, :937-940) are read
-  // only by lanes whose water table is below the column: a wave with none
-  // skips them (wave-uniform); the deepening loop's rare fall-through below
-  // the column then evaluates s_y(L) itself.
-  const bool any_aq = any_lane(aq);
-  FV<1> pA{{one}}, pY{{one}};
-  FV<2> eA{{zero, zero}}, eS{{zero, zero}};
-  if (any_aq) {
-  sp.template pick<1>(
-      [&](int h) __attribute__((always_inline)) -> FV<1> {
-        const float npsi = -PSI(L);
-        const float num = sel(h, aq ? (-PSI(L) + zwtmm - g.zi(L)) : npsi, zwtmm);
-        const float q = divr<CS::kRecip>(m, num, npsi, [&]() { return lay_d(cs, PF_RPSI0, L); });
-        const float ninv = LAYF(PF_NINVB, L);
-        return FV<1>{{m.powf(sel(h, q, one + q), sel(h, one + ninv, ninv))}};
-      },
-      pA, pY);
-  {
-    const float d0 = aq ? (zwtmm - g.zi(L)) : one;
-    float ve = LAYF(PF_PTE, L) / d0 * (1.0f - pA.v[0]);
-    ve = MAXF(ve, 0.0f);
-    ve = MINF(TS(L), ve);
-    sp.template pick<2>(
-        [&](int h) __attribute__((always_inline)) -> FV<2> {
-          // the quotient's and the power's checks deferred to one branch
-          // (round 2's d878d3e, backed out after a GPU fault that the calls
-          // of the then out-of-line redo caused: DESIGN.md §3)
-          const float xn = sel(h, ve, theta[L]);
-          auto xof = [&](float q2) __attribute__((always_inline)) {
-            float sn = MAXX(0.5f * (one + q2), 0.01f);
-            sn = MINC(one, sn);
-            const float x = sel(h, MAXX(q2, 0.01f), sn);
-            return aq ? x : one;
-          };
-          bool sq = false, sw = false;
-          float q2 = divr_d<CS::kRts>(m, xn, TS(L), [&]() { return lay_d(cs, PF_RTS0, L); }, sq);
-          float x = xof(q2);
-          float pw = m.powf_d(x, -BSW(L), sw);
-          if (__builtin_expect(sq | sw, 0)) {
-            divr_fix<CS::kRts>(m, q2, xn, TS(L));
-            x = xof(q2);
-            pw = m.powf(x, -BSW(L));
-          }
-          float z = PSI(L) * pw;
-          z = MAXC(smpmin, z);
-          return FV<2>{{z, -BSW(L) * z / (x * TS(L))}};
-        },
-        eA, eS);
-  }
-  }  // any_aq
-  zq[L + 1] = aq ? eA.v[0] : zero;
-  const float smp1 = eS.v[0], dsmpdw1 = eS.v[1];
-  cs.launder();
-  pr.mark(2);
-
-  // :598-639 conductivity and matric potential, own layers
-  float hk[L + 1], dhkdw[L + 1], dsmpdw[L + 1];
-  {
-    float *const out[4] = {hk, dhkdw, smp, dsmpdw};
     auto hk_exact = [&](int t, int h) __attribute__((always_inline)) -> FV<4> {
+          H9G_BR(BR_HKX);
           const int i0 = 2 * t + 1;
           const int ip1 = (L < i0 + 2) ? L : i0 + 2;          // ip of layer i0+1
           const float th = sel(h, theta[i0], theta[i0 + 1]);
@@ -958,8 +908,6 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           float s1 = 0.5f * (th + thp) / (0.5f * (ts + tsp));
           s1 = MINC(one, s1);
           const float bsw = OWN(PF_BSW);
-          // (s_node from the reciprocal only with room to spare in VGPRs: +35
-          // spilled VGPRs at 168, measured)
           float s_node = MAXX(divr<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }),
                               0.01f);
           s_node = MINC(one, s_node);
@@ -1011,8 +959,71 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           r.v[3] = (-bsw) * sm / (s_node * ts);
           return r;
     };
-    sp.template par_d<NT, 4, H9G_FE_HK>(hk_fast, hk_exact, out);
+    // (round 3: the two phases' slots interleaved in one region, twice the
+    // independent powers per region, spilled 225 VGPRs: 214.5 vs 208.9 ms)
+    sp.template par_d<NT, 1, H9G_FE_EQ>(eq_fast, eq_exact, outq);
+    pr.mark(2);
+    sp.template par_d<NT, 4, H9G_FE_HK>(hk_fast, hk_exact, outk);
   }
+  // Four single powers split over the pair (unused ones get base 1):
+  //   lane 0: temp0 of the aquifer node (:579-580), then zq(L+1) (:581-590);
+  //   lane 1: the specific-yield power of layer L (:937-940), then smp1 of
+  //           the aquifer row (:737-741).
+  // The aquifer node's powers and row (:574-590, :737-741, :937-940) are read
+  // only by lanes whose water table is below the column: a wave with none
+  // skips them (wave-uniform); the deepening loop's rare fall-through below
+  // the column then evaluates s_y(L) itself.
+  const bool any_aq = any_lane(aq);
+  FV<1> pA{{one}}, pY{{one}};
+  FV<2> eA{{zero, zero}}, eS{{zero, zero}};
+  if (any_aq) {
+  H9G_BR(BR_ANYAQ);
+  sp.template pick<1>(
+      [&](int h) __attribute__((always_inline)) -> FV<1> {
+        const float npsi = -PSI(L);
+        const float num = sel(h, aq ? (-PSI(L) + zwtmm - g.zi(L)) : npsi, zwtmm);
+        const float q = divr<CS::kRecip>(m, num, npsi, [&]() { return lay_d(cs, PF_RPSI0, L); });
+        const float ninv = LAYF(PF_NINVB, L);
+        return FV<1>{{m.powf(sel(h, q, one + q), sel(h, one + ninv, ninv))}};
+      },
+      pA, pY);
+  {
+    const float d0 = aq ? (zwtmm - g.zi(L)) : one;
+    float ve = LAYF(PF_PTE, L) / d0 * (1.0f - pA.v[0]);
+    ve = MAXF(ve, 0.0f);
+    ve = MINF(TS(L), ve);
+    sp.template pick<2>(
+        [&](int h) __attribute__((always_inline)) -> FV<2> {
+          // the quotient's and the power's checks deferred to one branch
+          // (round 2's d878d3e, backed out after a GPU fault that the calls
+          // of the then out-of-line redo caused: DESIGN.md §3)
+          const float xn = sel(h, ve, theta[L]);
+          auto xof = [&](float q2) __attribute__((always_inline)) {
+            float sn = MAXX(0.5f * (one + q2), 0.01f);
+            sn = MINC(one, sn);
+            const float x = sel(h, MAXX(q2, 0.01f), sn);
+            return aq ? x : one;
+          };
+          bool sq = false, sw = false;
+          float q2 = divr_d<CS::kRts>(m, xn, TS(L), [&]() { return lay_d(cs, PF_RTS0, L); }, sq);
+          float x = xof(q2);
+          float pw = m.powf_d(x, -BSW(L), sw);
+          if (__builtin_expect(sq | sw, 0)) {
+            H9G_BR(BR_AQS);
+            divr_fix<CS::kRts>(m, q2, xn, TS(L));
+            x = xof(q2);
+            pw = m.powf(x, -BSW(L));
+          }
+          float z = PSI(L) * pw;
+          z = MAXC(smpmin, z);
+          return FV<2>{{z, -BSW(L) * z / (x * TS(L))}};
+        },
+        eA, eS);
+  }
+  }  // any_aq
+  zq[L + 1] = aq ? eA.v[0] : zero;
+  const float smp1 = eS.v[0], dsmpdw1 = eS.v[1];
+  cs.launder();
   pr.mark(3);
   // :645-650 aquifer node geometry
   const float zcA = 0.5f * (zwtmm + g.zc(L));
@@ -1086,6 +1097,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     }
     // fluxes made exact here, so the layer arrays die before the sweep
     if (__builtin_expect(bad, 0)) {
+      H9G_BR(BR_TRIFLUX);
 #pragma unroll
       for (int i = 1; i <= L; i++) {
         const bool a = i == L;
@@ -1133,6 +1145,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     const float rmA = qo[L] - zero;
     row_f(L + 1, aq ? -d1[L] : zero, aq ? bmA : qA, zero, aq ? rmA : zero);
     if (__builtin_expect(bad | zp | (bm1 == 0.0f), 0)) {  // the exact sweep on the (exact) fluxes
+      H9G_BR(BR_TRISWEEP);
       BET = zero;
       zero_pivot = 0;
       const float bm1x = m.div(g.dz(1), dt, g.rdt()) + d1[1];
@@ -1237,6 +1250,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // independent: one lane of the pair evaluates each.
   float qcharge, sy_first = zero;
   if (jwt < L) {
+    H9G_BR(BR_JWTCOL);
     // operands of layer jwt+1 (and jwt): the parameters by runtime-indexed
     // store reads, the register arrays by selects
     const int j1 = jwt + 1;
@@ -1261,6 +1275,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           const float e = sel(h, 2.0f * bsw_j + 3.0f, cs.lay(PF_NINVB, j1));
           float w = m.powf_d(h ? one + q : s1, e, sw);
           if (__builtin_expect((h && sq) | sw, 0)) {          // one deferred check
+            H9G_BR(BR_RECH);
             divr_fix<CS::kRecip>(m, q, zwtmm, nb);
             w = m.powf(h ? one + q : s1, e);
           }
@@ -1341,6 +1356,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
         float q = divr_d<CS::kRecip>(m, zwtmm, nb, [&]() { return lay_d(cs, PF_RPSI0, i); }, sq);
         float w = m.powf_d(one + q, cs.lay(PF_NINVB, i), sw);
         if (__builtin_expect(se | sq | sw, 0)) {
+          H9G_BR(BR_BASE);
           if (se) ex = m.expf(-fff * s.zwt);
           divr_fix<CS::kRecip>(m, q, zwtmm, nb);
           w = m.powf(one + q, cs.lay(PF_NINVB, i));
@@ -1409,6 +1425,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
 #pragma unroll
   for (int i = 1; i <= L; i++) low |= h2o[i] < watmin;
   if (__builtin_expect(low | m.div_bad(qflx_rsub_sat), 0)) {
+  H9G_BR(BR_WATMIN);
   m.div_fix(qflx_rsub_sat, xs1, dt);
   // :1161-1174 watmin top-down
 #pragma unroll
@@ -1531,6 +1548,10 @@ template <int L, class G, class SP, class CS, class PR>
 H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_sum, float &errval,
                         const h9m::Tabs &T, PR &pr, int ns) {
   pr.mark(0);
+  H9G_BR(BR_SUBSTEP);
+#if defined(H9G_ISA_MARK) && defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("; h9g-substep");     // tools/isa_mix.py: once per substep
+#endif
   MathFast mf{T, false};
 #if defined(H9G_FORCE_RERUN)
   const bool in_column = s.zwt <= g.zim(L);   // the substeps that may re-run (cell_year_pair)
@@ -1543,6 +1564,7 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
   if (in_column && ns % H9G_FORCE_RERUN == H9G_FORCE_RERUN - 1) mf.special = true;
 #endif
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
+    H9G_BR(BR_RERUN);
 #if defined(H9G_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)
     atomicAdd(&h9g_exact_count, 1ull);      // measurement builds only
     atomicAdd(&h9g_exact_wave[(blockIdx.x * 4 + (threadIdx.x >> 6)) & 0xffff], 1u);
@@ -1593,8 +1615,10 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
   float npp = zero;
   int code = 0;
   MathExact me{T};
+  s.naq = 0;
   for (int day = 0; day < nt; day++) {
     cs.day_start(day);
+    H9G_BR(BR_DAY);
     cs.launder();
     opaque(A);
     const gbl_float *f = forc + (size_t)day * fday;
@@ -1624,7 +1648,10 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
       // the day snapshot, taken before the first substep of the day whose
       // water table is in the column (jwt < L): only such a substep visits
       // layers (:923-1118), so only it can need the exact re-run
-      if (!snapped && s.zwt <= g.zim(L)) {
+      const bool in_column = s.zwt <= g.zim(L);
+      s.naq += in_column ? 0 : 1;
+      if (!snapped && in_column) {
+        H9G_BR(BR_SNAP);
         save_day<L>(sp, cs, s, rnf_sum, ns);
         snapped = true;
       }

@@ -119,6 +119,30 @@ H9K_HD bool any_lane(bool p) {
 #endif
 }
 
+// Branch counters (measurement builds, -DH9G_COUNT_BRANCH; tools/isa_mix.py
+// weighs the static mix with them): H9G_BR(k) counts the waves that enter
+// site k ([k]) and their active lanes ([32 + k]).  Empty in product builds.
+#if defined(H9G_COUNT_BRANCH)
+__device__ unsigned long long h9g_branch_count[64];
+#endif
+#if defined(H9G_COUNT_BRANCH) && defined(__HIP_DEVICE_COMPILE__)
+#define H9G_BR(k)                                                                   \
+  do {                                                                              \
+    const uint64_t em_ = __builtin_amdgcn_read_exec();                              \
+    if (__lane_id() == (unsigned)__builtin_ctzll(em_)) {                            \
+      atomicAdd(&h9g_branch_count[(k)], 1ull);                                      \
+      atomicAdd(&h9g_branch_count[32 + (k)], (unsigned long long)__builtin_popcountll(em_)); \
+    }                                                                               \
+  } while (0)
+#else
+#define H9G_BR(k) ((void)0)
+#endif
+enum : int {   // H9G_BR sites
+  BR_SUBSTEP = 0, BR_THETA, BR_QB, BR_EQX, BR_AQPOW, BR_AQS, BR_HKX, BR_TRIFLUX, BR_TRISWEEP, BR_RECH,
+  BR_BASE, BR_WATMIN, BR_RERUN, BR_POWREDO, BR_DIVREDO, BR_EXPREDO, BR_POWFIX, BR_DIVFIX, BR_INL, BR_ANYAQ,
+  BR_JWTCOL, BR_VISIT2, BR_SNAP, BR_DAY, BR_N
+};
+
 // ------------------------------------------------------------ math policies
 // A fast-division quotient that must re-run exactly: subnormal (RN32 of the
 // double product may differ from the correctly rounded quotient there) or
@@ -207,6 +231,7 @@ struct MathFast {
     bool sp = false;
     float r = h9m::expf_nx(x, T, sp);
     if (__builtin_expect(sp, 0)) {
+      H9G_BR(BR_EXPREDO);
       r = expf_redo(x, T.exp2, T.log2);
       redone++;
     }
@@ -216,6 +241,7 @@ struct MathFast {
     bool sp = false;
     float r = h9m::powf_nx<false>(x, y, T, sp);
     if (__builtin_expect(sp, 0)) {
+      H9G_BR(BR_POWREDO);
       r = powf_redo(x, y, T.exp2, T.log2);
       redone++;
     }
@@ -228,6 +254,7 @@ struct MathFast {
   H9K_HD float div(float x, float d, double r) {
     float q = (float)((double)x * r);
     if (__builtin_expect(bad_quotient(q), 0)) {
+      H9G_BR(BR_DIVREDO);
       q = x / d;
       redone++;
     }
@@ -247,6 +274,7 @@ struct MathFast {
   }
   H9K_HD void powf_fix(float &r, float x, float y, bool sp) {
     if (sp) {
+      H9G_BR(BR_POWFIX);
       r = powf_redo(x, y, T.exp2, T.log2);
       redone++;
     }
@@ -255,6 +283,7 @@ struct MathFast {
   H9K_HD bool div_bad(float q) const { return bad_quotient(q); }
   H9K_HD void div_fix(float &q, float x, float d) {
     if (bad_quotient(q)) {
+      H9G_BR(BR_DIVFIX);
       q = x / d;
       redone++;
     }
@@ -312,6 +341,8 @@ template <int L>
 struct St {            // persistent per-cell state (SHARED.f90), in registers
   float h2o[L + 1], smp[L + 1];
   float zwt, wa, LAI, LAI_litter, pm, pfm, plen, rdepth;
+  int naq;             // substeps of the year with the water table below the column
+                       // (not model state: the next year's cell order, h9g_sort_kernel)
 };
 
 struct Day {           // HYBRID9.f90:168-184 + forcing read by HYDROLOGY
