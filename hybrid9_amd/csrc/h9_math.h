@@ -143,14 +143,26 @@ H9_HD int checkint(uint32_t iy) {
 
 H9_HD bool zeroinfnan(uint32_t ix) { return 2 * ix - 1 >= 2u * 0x7f800000 - 1; }
 
+// x is a positive normal float: asuint(x) - 0x00800000 < 0x7f800000 - 0x00800000
+H9_HD bool is_pos_normal(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_classf(x, 0x100);      // +normal
+#else
+  return asu32(x) - 0x00800000u < 0x7f800000u - 0x00800000u;
+#endif
+}
+
 H9_HD double log2_inline(uint32_t ix, const Tabs &T) {
   const uint32_t tmp = ix - 0x3f330000u;
-  const int i = (tmp >> 19) % 16;
+  // i = (tmp >> 19) % 16; the {invc, logc} pair at byte offset 16 i (two
+  // shifts-and-masks as one: (tmp >> 15) & 0xf0)
+  const uint32_t off = (tmp >> 15) & 0xf0u;
   const uint32_t top = tmp & 0xff800000u;
   const uint32_t iz = ix - top;
   const int k = (int32_t)top >> 23;
-  const double invc = T.log2[2 * i];
-  const double logc = T.log2[2 * i + 1];
+  const double *tc = (const double *)((const char *)T.log2 + off);
+  const double invc = tc[0];
+  const double logc = tc[1];
   const double z = (double)asf32(iz);
   const double r = fma_d(z, invc, -1.0);
   const double y0 = logc + (double)k;
@@ -246,11 +258,12 @@ H9_HD float powf_nx(float x, float y, const Tabs &T, bool &special) {
   const double logx = log2_inline(ix, T);
   const double ylogx = (double)y * logx;
   // (| on bools: evaluate every test, no branches)
-  // |y log2 x| >= 126 on the high word: ((bits >> 47) & 0xffff) >= 0x80bf
-  // <=> (hi & 0x7fff8000) >= 0x405f8000 (a 32-bit compare, not 64-bit)
-  const uint32_t hi = (uint32_t)(asu64(ylogx) >> 32);
-  special |= (int)(ix - 0x00800000u >= 0x7f800000u - 0x00800000u) | (int)(CheckY && zeroinfnan(iy)) |
-             (int)((hi & 0x7fff8000u) >= 0x405f8000u);
+  // glibc's (asuint64(ylogx) >> 47 & 0xffff) >= asuint64(126.0) >> 47 compares
+  // |ylogx|'s bits, truncated below bit 47, with 126.0's (whose bits below 47
+  // are zero): |ylogx| >= 126 or NaN, i.e. !(|ylogx| < 126) -- one f64
+  // compare.  x outside [2^-126, 2^128) or negative: ix - 0x00800000 >=
+  // 0x7f000000, i.e. x is not a positive normal number -- one class test.
+  special |= (int)!is_pos_normal(x) | (int)(CheckY && zeroinfnan(iy)) | (int)!(__builtin_fabs(ylogx) < 126.0);
   return exp2_inline(ylogx, 0, T);
 }
 

@@ -762,6 +762,7 @@ struct h9g_ctx {
   int *d_slow = nullptr;
   float *d_sv = nullptr;          // pair kernel rollback blocks
   int *d_perm = nullptr;          // cell order of the year kernel (h9g_sort_kernel)
+  unsigned *d_aqbits = nullptr;   // H9G_DUMP_AQ builds: day-level water-table record of the last year
   int *d_hist = nullptr;          // per cell: substeps of the last year below the column (-1: none)
   int hist_nsub = 0;              // substeps of that year
   unsigned *d_pace = nullptr;     // Pacer mode 2 progress rows (h9g_pair.h)
@@ -866,6 +867,7 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_slow);
   (void)hipFree(ctx->d_perm);
   (void)hipFree(ctx->d_hist);
+  (void)hipFree(ctx->d_aqbits);
   (void)hipFree(ctx->d_pace);
   for (auto e : ctx->ev_copied) hipEventDestroy(e);
   for (auto e : ctx->ev_consumed) hipEventDestroy(e);
@@ -1300,6 +1302,29 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
     }
     ctx->nev = 0;
   }
+#if defined(H9G_DUMP_AQ)
+  // the last year's record to $H9G_AQ_DUMP: year, n, then n x 12 words
+  if (const char *path = getenv("H9G_AQ_DUMP"); path && ctx->d_aqbits && ctx->ran) {
+    std::vector<unsigned> bits(12 * ctx->n);
+    HIPCHK(hipStreamSynchronize(ctx->sc));
+    HIPCHK(hipMemcpy(bits.data(), ctx->d_aqbits, sizeof(unsigned) * bits.size(), hipMemcpyDeviceToHost));
+    if (FILE *f = fopen(path, "ab")) {
+      const int hdr[2] = {ctx->last_year, (int)ctx->n};
+      fwrite(hdr, sizeof(int), 2, f);
+      fwrite(bits.data(), sizeof(unsigned), bits.size(), f);
+      fclose(f);
+    }
+  }
+  if (!ctx->d_aqbits) HIPCHK(hipMalloc(&ctx->d_aqbits, sizeof(unsigned) * 12 * ctx->n));
+  HIPCHK(hipMemsetAsync(ctx->d_aqbits, 0, sizeof(unsigned) * 12 * ctx->n, ctx->sc));
+  {
+    const float *base = ctx->d_ann;
+    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(h9g_aq_bits), &ctx->d_aqbits, sizeof(void *), 0,
+                                  hipMemcpyHostToDevice, ctx->sc));
+    HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(h9g_aq_base), &base, sizeof(void *), 0, hipMemcpyHostToDevice,
+                                  ctx->sc));
+  }
+#endif
   const int e = ctx->nev++;
   HIPCHK(hipEventRecord(ctx->ev0[e], ctx->sc));
   if (ctx->kind == 2) {

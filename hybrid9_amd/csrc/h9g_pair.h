@@ -1619,6 +1619,12 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
   for (int day = 0; day < nt; day++) {
     cs.day_start(day);
     H9G_BR(BR_DAY);
+#if defined(H9G_DUMP_AQ) && defined(__HIP_DEVICE_COMPILE__)
+    if (h9g_aq_bits && s.zwt > g.zim(L)) {
+      const size_t c = (size_t)((const float *)acc - h9g_aq_base);
+      atomicOr(&h9g_aq_bits[c * 12 + day / 32], 1u << (day & 31));
+    }
+#endif
     cs.launder();
     opaque(A);
     const gbl_float *f = forc + (size_t)day * fday;

@@ -137,6 +137,13 @@ __device__ unsigned long long h9g_branch_count[64];
 #else
 #define H9G_BR(k) ((void)0)
 #endif
+// Day-level water-table record (measurement builds, -DH9G_DUMP_AQ; tools/
+// aq_sort.py designs the cell order from it): bit d of h9g_aq_bits[c][d/32]
+// = the water table of cell c is below the column at the start of day d.
+#if defined(H9G_DUMP_AQ)
+__device__ unsigned *h9g_aq_bits;
+__device__ const float *h9g_aq_base;   // the annual array: cell = acc - base
+#endif
 enum : int {   // H9G_BR sites
   BR_SUBSTEP = 0, BR_THETA, BR_QB, BR_EQX, BR_AQPOW, BR_AQS, BR_HKX, BR_TRIFLUX, BR_TRISWEEP, BR_RECH,
   BR_BASE, BR_WATMIN, BR_RERUN, BR_POWREDO, BR_DIVREDO, BR_EXPREDO, BR_POWFIX, BR_DIVFIX, BR_INL, BR_ANYAQ,
