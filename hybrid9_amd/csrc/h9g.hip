@@ -11,8 +11,9 @@
 //     lanes.  22 columns per wave, 4 waves per workgroup: 3 waves on every
 //     SIMD at 0.5 deg (767 workgroups, 768 slots).  The column's water
 //     state lives in VGPRs, its read-mostly data (soil parameters and
-//     their invariants, rootr, the day's constants, the substep rollback
-//     copy) in the pair's two columns of an LDS block.  HBM traffic per
+//     their invariants, rootr, the day's constants) in the pair's two
+//     columns of an LDS block, the day snapshot of the exact re-run in an
+//     L2-resident global block.  HBM traffic per
 //     cell-day is the 7 forcing values (coalesced, cell-fastest) plus the
 //     annual sums (L2-resident): the SHARED-state contract of each substep
 //     (376 B at L=8) never leaves the CU.
@@ -76,7 +77,7 @@ struct KArgs {
   int *__restrict__ err;           // 4 rows x ncell: code, day, substep, value bits
   int *__restrict__ err_flag;
   unsigned *__restrict__ stamps;   // H9G_STAMPS builds: 8 phase cycle sums per wave
-  float *__restrict__ sv;          // pair kernel: substep rollback, PairStore::GBLOCK bytes per workgroup
+  float *__restrict__ sv;          // pair kernel: day snapshot, PairStore::GBLOCK bytes per workgroup
   const int *__restrict__ perm;    // lane slot -> cell (h9g_sort_kernel), or null: identity
   int *__restrict__ hist;          // per cell: substeps of the year with the water table below the column
   unsigned *__restrict__ pace;     // pair kernel, Pacer mode 2: H9G_PACE_ROWS x 16 progress words
@@ -760,7 +761,7 @@ struct h9g_ctx {
   float soil_ms = 0.0f;           // device time of the last h9g_soil_layer
   int soil_slow = 0;              // cells of the last layer summed in the reference's order
   int *d_slow = nullptr;
-  float *d_sv = nullptr;          // pair kernel rollback blocks
+  float *d_sv = nullptr;          // pair kernel day-snapshot blocks
   int *d_perm = nullptr;          // cell order of the year kernel (h9g_sort_kernel)
   unsigned *d_aqbits = nullptr;   // H9G_DUMP_AQ builds: day-level water-table record of the last year
   int *d_hist = nullptr;          // per cell: substeps of the last year below the column (-1: none)
@@ -910,7 +911,7 @@ static int l10_kind(size_t n, int ncu, size_t *n_solo) {
 
 // Device bytes a context of this configuration allocates: h9g_create's
 // arrays plus what the first h9g_run_year / h9g_soil_layer allocate lazily
-// (the pair kernel's per-workgroup rollback blocks, the pacing rows, the
+// (the pair kernel's per-workgroup day-snapshot blocks, the pacing rows, the
 // soil build's slow-cell flags).
 size_t h9g_config_bytes(const h9g_config *cfg) {
   if (!cfg || cfg->ncell <= 0 || cfg->nlayers < 1 || cfg->max_days < 1 || cfg->nslots < 1) return 0;

@@ -52,7 +52,7 @@ enum : int {
   PF_ROOTR,                            // rootr_col(1..L)
   PF_RPSI0, PF_RPSI1,                  // 1/(-psi), double (recip64) low, high word   (kRecip)
   PF_RTS0, PF_RTS1,                    // 1/theta_s, double                           (kRts)
-  PF_SVH2O, PF_SVSMP,                  // substep rollback (sv_* of the store)
+  PF_SVH2O, PF_SVSMP,                  // day snapshot (sv_* of the store)
   PF_N
 };
 // per-cell fields
@@ -124,7 +124,7 @@ H9K_HD float hi_d(double v) {
 // Every store has the same interface: lay/set_lay (per-layer field p of
 // layer i), sc/set_sc (per-cell field k), slot/set_slot (own layer t of a
 // pair lane), day/set_day, the day reciprocals day_r/set_day_r, and the
-// substep rollback sv_* (q = 0: h2osoi_liq, 1: smp; k = SV_*).  kRecip,
+// day snapshot sv_* (q = 0: h2osoi_liq, 1: smp; k = SV_*).  kRecip,
 // kRts, kDayRecip say which reciprocal fields it holds (LDS budget).
 template <int L>
 struct FlatStore {                     // host: one flat array per cell
@@ -171,9 +171,9 @@ struct FlatStore {                     // host: one flat array per cell
 // spread the same way over the two columns.  Both lanes of a pair store
 // identical values to the same address where they both write.
 //
-// The substep rollback lives in global memory (L2-resident: 76 B per
+// The day snapshot lives in global memory (L2-resident: 80 B per
 // cell), in a per-workgroup block shaped like the LDS block: the byte
-// offset of a value is its LDS address, so every rollback store is
+// offset of a value is its LDS address, so every snapshot store is
 // `global_store v_lds_address, s_block + imm` with no address arithmetic.
 // That leaves LDS room, within 3 workgroups per CU (76 rows per wave), for
 // the reciprocal fields: 1/(-psi) at any L, 1/theta_s and the day
@@ -263,7 +263,7 @@ struct PairStore {
   static constexpr int GBLOCK = 65536;                      // bytes per workgroup (>= any LDS address)
   lds_float *self, *even;
   const lds_float *zt;                 // zi(0..L+1), then zi(0..L+1)/1000 (per block)
-  float *svw;                          // this workgroup's rollback block (global)
+  float *svw;                          // this workgroup's day-snapshot block (global)
   static constexpr int RESIDENT = pair_resident<L>();       // workgroups per CU = waves per SIMD (h9g.hip pair_waves)
   Pacer pace;
   __device__ __forceinline__ void day_start(int day) const { pace.day_start(day, RESIDENT); }
@@ -313,7 +313,7 @@ struct PairStore {
   }
   __device__ __forceinline__ float root(int i) const { return lay(PF_ROOTR, i); }
   __device__ __forceinline__ void set_root(int i, float v) const { set_lay(PF_ROOTR, i, v); }
-  // rollback: rows q*NT + t (layers), 2*NT + k/2 (scalars) of the global block
+  // snapshot: rows q*NT + t (layers), 2*NT + k/2 (scalars) of the global block
   __device__ __forceinline__ float *gl(const lds_float *p, int off) const {
     return (float *)((char *)svw + (uint32_t)(size_t)p) + off;
   }
@@ -338,7 +338,7 @@ struct PairStore {
 
 // Device, one lane per column ("solo"): column `lane` of a [row][64] block,
 // every field in the lane's own column; no reciprocal fields, no parking
-// (1054 waves = 5 blocks/CU), rollback in LDS.
+// (1054 waves = 5 blocks/CU), day snapshot in LDS.
 template <int L>
 struct SoloStore {
   static constexpr bool kRecip = false, kRts = false, kDayRecip = false, kRtsHK = false;

@@ -30,8 +30,8 @@
 // (deferred-check forms *_d / *_fix: one branch per group of independent
 // operations).  MathExact evaluates glibc's full logic and divides.  Results
 // are bit-identical either way.  Only a water-table loop that needs a third
-// layer visit re-runs its substep, exactly, from the rollback copy
-// (h9g_pair.h substep_pair).
+// layer visit re-runs its substep, exactly, replaying the day from its
+// snapshot (h9g_pair.h save_day / substep_exact_pair).
 #pragma once
 #include "h9_math.h"
 #include "h9g_geo.h"

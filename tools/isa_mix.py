@@ -136,10 +136,8 @@ def classify(op: str) -> str:
     return "pseudo." + op
 
 
-def main() -> None:
-    stem = Path(sys.argv[1])
-    pos = [a for a in sys.argv[2:] if not a.startswith("--")]
-    func = pos[0] if pos else "_Z15h9g_pair_kernelILi8EN3h9k4GeoCILi8ELi48EEEEv5KArgsT0_"
+def weights(stem: Path, func: str, argv=()):
+    """per-block frequency per wave-substep and the substep loop's blocks"""
     blocks, succ = parse(stem.with_suffix(".mir").read_text(), func)
     n = max(blocks) + 1
     rows, cols, vals = [], [], []
@@ -152,7 +150,6 @@ def main() -> None:
     e = np.zeros(n)
     e[0] = 1.0
     f = spl.spsolve((sp.identity(n, format="csr") - P).tocsc(), e)
-    # substep loop header: innermost loop header (assembly comments) of largest frequency
     asm = stem.with_suffix(".s").read_text()
     asm = asm[asm.index(f"{func}:"):]
     asm = asm[:asm.index(".Lfunc_end")]
@@ -165,14 +162,13 @@ def main() -> None:
         if m and last is not None:
             hdr.append((last, int(m.group(1))))
     hdr = [h for h in hdr if h[0] in blocks]
-    if "--headers" in sys.argv:
+    if "--headers" in argv:
         for b, d in hdr:
             print(f"  header bb.{b} depth {d} freq {f[b]:.4g} instrs {len(blocks[b])}")
-    hsel = [a for a in sys.argv[2:] if a.startswith("--header=")]
+    hsel = [a for a in argv if a.startswith("--header=")]
     h = int(hsel[0].split("=")[1]) if hsel else max(hdr, key=lambda x: (x[1] == 2, f[x[0]]))[0]
     mark = sum(f[b] for b, ins in blocks.items() for op in ins if op == "MARK")
     w = f / (mark if mark > 0 else f[h])
-    # blocks of that loop (its own and nested loops'), from the loop comments
     inloop, last = set(), None
     tag = re.compile(rf"(Header=BB\d+_{h}\b|Parent Loop BB\d+_{h}\b)")
     for line in asm.splitlines():
@@ -183,6 +179,14 @@ def main() -> None:
                 inloop.add(last)
         if last is not None and tag.search(line):
             inloop.add(last)
+    return {b: w[b] for b in blocks}, inloop, blocks, h, mark
+
+
+def main() -> None:
+    stem = Path(sys.argv[1])
+    pos = [a for a in sys.argv[2:] if not a.startswith("--")]
+    func = pos[0] if pos else "_Z15h9g_pair_kernelILi8EN3h9k4GeoCILi8ELi48EEEEv5KArgsT0_"
+    w, inloop, blocks, h, mark = weights(stem, func, sys.argv[2:])
     mix, ops = Counter(), Counter()
     for b, ins in blocks.items():
         if b not in inloop:
