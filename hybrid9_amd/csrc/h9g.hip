@@ -885,28 +885,22 @@ void h9g_destroy(h9g_ctx *ctx) {
 }
 
 // Kernel for L = 10 (1: pair, 2: solo, 3: both).  They are bit-identical
-// and differ in how n columns quantise into rounds of resident waves.  The
-// solo kernel (1-wave blocks, 1 wave/SIMD: its 36.6 KB LDS column store
-// allows four per CU) packs 64 columns per wave; the pair kernel
-// (88-column blocks, 3 waves/SIMD, pair_resident) 22.  Time per round
-// measured on config 5 (270,000 columns, 1 GPU, round 3): solo 659 ms / 5,
-// pair 535 ms / 4.  Kind 3 runs the whole solo rounds and hands the
-// remainder (less than one solo round) to the pair kernel.  Returns the kind
-// and sets *n_solo (cells [0, n_solo) on the solo kernel, for kind 3).
+// and differ in how n columns quantise into rounds of resident waves: the
+// solo kernel (1-wave blocks, 1 wave/SIMD) packs 64 columns per wave, the
+// pair kernel (88-column blocks, 3 waves/SIMD since round 3, pair_resident)
+// 22; kind 3 runs the whole solo rounds and the pair kernel on the rest.
+// Round 3 measured every strong-scaling shard of the config-5 grid
+// (tools/l10_shards.py, profiles/r03e_l10_shards.txt, ms per year, pair /
+// solo / mixed): 270,000 cells 537.7 / 618.6 / 538.1; 135,000 274.5 / 373.2 /
+// 274.4; 67,500 130.1 / 246.5 / 130.4; 33,750 107.9 / 134.1 / 108.1.  The
+// pair kernel is within noise of the best everywhere, so it is the choice;
+// round 2's rounds model picked solo at 33,750 cells (24% slower there).
+// Solo and mixed stay selectable (H9G_KERNEL) and are tested.  *n_solo:
+// the whole solo rounds (kind 3 only).
 static int l10_kind(size_t n, int ncu, size_t *n_solo) {
-  const size_t per_pair = (size_t)H9G_PCPW * H9G_PWAVES, solo_round = (size_t)4 * ncu * H9G_YBLOCK;
-  const size_t pair_slots = (size_t)pair_resident<10>() * ncu;
-  auto pair_rounds = [&](size_t m) { return ((m + per_pair - 1) / per_pair + pair_slots - 1) / pair_slots; };
-  const size_t rs = (n + solo_round - 1) / solo_round;
-  const size_t t_solo = rs * 1318, t_pair = pair_rounds(n) * 1338;
-  const size_t full = n / solo_round;
-  const size_t t_mixed = full * 1318 + pair_rounds(n - full * solo_round) * 1338;
-  *n_solo = 0;
-  if (full >= 1 && n > full * solo_round && t_mixed < t_solo && t_mixed < t_pair) {
-    *n_solo = full * solo_round;
-    return 3;
-  }
-  return t_solo <= t_pair ? 2 : 1;
+  const size_t solo_round = (size_t)4 * ncu * H9G_YBLOCK;
+  *n_solo = (n / solo_round) * solo_round;
+  return 1;
 }
 
 // Device bytes a context of this configuration allocates: h9g_create's

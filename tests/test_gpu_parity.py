@@ -211,8 +211,8 @@ def test_config2_full_grid_sampled_against_oracle():
 @pytest.mark.parametrize("kernel", ["pair", "solo", "mixed"])
 def test_config5_l10_quarter_degree_sample(kernel, monkeypatch):
     """10 soil layers (config 5) on 0.25 deg cells, NS=24, GROW on, both
-    year kernels and the mixed launch (the L=10 choice follows the column
-    count, h9g.hip l10_kind), against the C restatement on 2,048 cells.  The
+    year kernels and the mixed launch (the default at L=10 is the pair kernel,
+    h9g.hip l10_kind), against the C restatement on 2,048 cells.  The
     restatement is itself pinned at L=10 to the reference's own L=10 build
     (oracle/_ref/h9ref_l10: SHARED.f90:294,300 set to 10/11) by the golden
     c5_l10_sample, which test_config5_l10_matches_reference_golden runs here."""
