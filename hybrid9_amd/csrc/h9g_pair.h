@@ -385,7 +385,24 @@ struct SoloStore {
 // flux(evg, tran) receives the substep's qflx_evap_grnd and
 // qflx_tran_veg_col (HYDROLOGY.f90:388-400); only the site path keeps them.
 struct NoProf {
+#if defined(H9G_ISA_PHASES) && defined(__HIP_DEVICE_COMPILE__)
+  template <int K>
+  __device__ __forceinline__ void markk() { asm volatile("; h9g-phase %0" ::"i"(K)); }   // tools/isa_mix.py --phases
+  H9K_HD void mark(int k) {
+    switch (k) {
+      case 0: markk<0>(); break;
+      case 1: markk<1>(); break;
+      case 2: markk<2>(); break;
+      case 3: markk<3>(); break;
+      case 4: markk<4>(); break;
+      case 5: markk<5>(); break;
+      case 6: markk<6>(); break;
+      default: markk<7>(); break;
+    }
+  }
+#else
   H9K_HD void mark(int) {}
+#endif
   H9K_HD void flux(float, float) {}
 };
 struct FluxProf {

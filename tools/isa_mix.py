@@ -68,6 +68,10 @@ def parse(mir: str, func: str):
         if op is not None and op.startswith("INLINEASM") and "h9g-substep" in line:
             blocks[cur].append("MARK")
             continue
+        if op is not None and op.startswith("INLINEASM") and "h9g-phase" in line:
+            m = re.search(r"\[imm\],\s*(\d+)", line)
+            blocks[cur].append("PHASE" + (m.group(1) if m else "?"))
+            continue
         if op is None or op == "BUNDLE" or op.startswith("INLINEASM") or op in ("DBG_VALUE", "KILL", "IMPLICIT_DEF",
                                                                                 "SCHED_BARRIER"):
             continue
@@ -187,12 +191,25 @@ def main() -> None:
     pos = [a for a in sys.argv[2:] if not a.startswith("--")]
     func = pos[0] if pos else "_Z15h9g_pair_kernelILi8EN3h9k4GeoCILi8ELi48EEEEv5KArgsT0_"
     w, inloop, blocks, h, mark = weights(stem, func, sys.argv[2:])
+    if "--phases" in sys.argv:
+        # blocks in layout (MIR number) order, each attributed to the last phase marker before it
+        phase, per = "?", defaultdict(Counter)
+        for b in sorted(blocks):
+            for op in blocks[b]:
+                if op.startswith("PHASE"):
+                    phase = op[5:]
+                    continue
+                if b in inloop and op not in ("MARK",):
+                    c = classify(op)
+                    per[phase]["valu" if c.startswith("valu") else c] += w[b]
+        for ph in sorted(per):
+            print(f"  phase {ph}: " + "  ".join(f"{k} {v:.0f}" for k, v in sorted(per[ph].items(), key=lambda x: -x[1]) if v >= 1))
     mix, ops = Counter(), Counter()
     for b, ins in blocks.items():
         if b not in inloop:
             continue
         for op in ins:
-            if op == "MARK":
+            if op == "MARK" or op.startswith("PHASE"):
                 continue
             c = classify(op)
             mix[c] += w[b]
