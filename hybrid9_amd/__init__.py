@@ -116,6 +116,7 @@ def lib() -> C.CDLL:
         "h9g_build_id": (C.c_char_p, []),
         "h9g_math_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP]),
         "h9g_div_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP, C.POINTER(C.c_int)]),
+        "h9g_pace_probe": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_uint)]),
         "h9g_math_fast_selftest": (C.c_int, [C.c_int, C.c_int, _FP, _FP, _FP, C.POINTER(C.c_int)]),
         "h9g_synth_host": (C.c_int, [C.c_uint64, C.c_int, C.c_int, _I64P, _FP, C.c_int,
                                      C.c_int, _FP, _FP]),

@@ -696,6 +696,29 @@ __global__ void h9g_soil_seq_kernel(int nx, int ncell, const int64_t *__restrict
 }
 
 // MathFast's division path with a device-computed reciprocal (recip64).
+// Probe of the hardware ids pace_key decodes (h9g_pair.h): the
+// pair kernel's launch shape and LDS footprint (dynamic LDS of the same size,
+// so the same workgroups per CU), each wave's lane 0 arriving at a bounded
+// barrier (s_sleep, at most `spin` shader cycles) and then recording
+// HW_REG_HW_ID, HW_REG_XCC_ID and whether every wave had arrived, i.e. was
+// resident at once.  out: 3 words per wave (blockIdx * waves + wave).
+__global__ void __launch_bounds__(64 * H9G_PWAVES) h9g_pace_probe_kernel(unsigned *out, unsigned *arrive,
+                                                                         unsigned total, long long spin) {
+  extern __shared__ float pad[];
+  if (threadIdx.x & 63) return;
+  pad[threadIdx.x] = 0.0f;
+  const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long t0 = clock64();
+  unsigned seen = 0;
+  while ((seen = __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < total &&
+         clock64() - t0 < spin)
+    __builtin_amdgcn_s_sleep(2);
+  out[3 * w + 0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);           // HW_REG_HW_ID
+  out[3 * w + 1] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;     // HW_REG_XCC_ID
+  out[3 * w + 2] = seen >= total ? 1u : 0u;
+}
+
 __global__ void h9g_div_kernel(int n, const float *x, const float *d, float *out, int *flag) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1787,6 +1810,24 @@ int h9g_math_fast_selftest(int device, int n, const float *x, const float *y, fl
   (void)hipFree(dy);
   (void)hipFree(dout);
   (void)hipFree(dflag);
+  return 0;
+}
+
+int h9g_pace_probe(int device, int nblocks, unsigned *out) {
+  if (nblocks <= 0 || !out) return H9G_EINVAL;
+  HIPCHK(hipSetDevice(device));
+  const size_t nw = (size_t)nblocks * H9G_PWAVES;
+  unsigned *dout = nullptr, *darr = nullptr;
+  HIPCHK(hipMalloc(&dout, sizeof(unsigned) * 3 * nw));
+  HIPCHK(hipMalloc(&darr, sizeof(unsigned)));
+  HIPCHK(hipMemset(darr, 0, sizeof(unsigned)));
+  const size_t lds = sizeof(float) * (size_t)PairStore<8, H9G_PLANES>::ROWS * H9G_PLANES * H9G_PWAVES +
+                     sizeof(uint64_t) * 32 + sizeof(double) * 32 + sizeof(float) * zt_size<8>();
+  h9g_pace_probe_kernel<<<nblocks, 64 * H9G_PWAVES, lds>>>(dout, darr, (unsigned)nw, 1ll << 29);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(out, dout, sizeof(unsigned) * 3 * nw, hipMemcpyDeviceToHost));
+  (void)hipFree(dout);
+  (void)hipFree(darr);
   return 0;
 }
 

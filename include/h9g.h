@@ -252,6 +252,10 @@ int h9g_math_fast_selftest(int device, int n, const float *x, const float *y,
  * the IEEE division (subnormal or NaN quotient). */
 int h9g_div_selftest(int device, int n, const float *x, const float *d,
                      float *out, int *flag);
+/* Hardware ids as the pair kernel's issue pacer decodes them: nblocks
+ * workgroups of the pair kernel's shape and LDS size; per wave out[3w..3w+2]
+ * = HW_REG_HW_ID, HW_REG_XCC_ID, 1 if every wave was resident at once. */
+int h9g_pace_probe(int device, int nblocks, unsigned *out);
 
 #ifdef __cplusplus
 }
