@@ -92,9 +92,12 @@ H9K_HD float MAXX(float x, float c) {
 // Scheduling fence: stops the machine scheduler from interleaving the
 // unrolled per-layer bodies (each a few powf with double-precision
 // temporaries), which otherwise multiplies the live register set by L.
+#ifndef H9G_FENCE_MASK
+#define H9G_FENCE_MASK 0x100   // kinds allowed to cross (sched.barrier mask): LDS reads (round 3: 200.8 -> 200.3 ms)
+#endif
 H9K_HD void sched_fence() {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(H9G_NOFENCE)
-  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(H9G_FENCE_MASK);
 #endif
 }
 

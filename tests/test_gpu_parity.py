@@ -208,6 +208,24 @@ def test_config2_full_grid_sampled_against_oracle():
     np.testing.assert_allclose(diag, hd, rtol=1e-12, atol=0)
 
 
+def test_config4_full_grid_30_years_sampled_against_oracle():
+    """Config 4 at its full size: the 0.5 deg grid (67,420 cells) spun up
+    over 1901-1930 (NS=48, GROW on) with the state carried in the device
+    context, 64 sampled cells bit-identical to the oracle after 30 years
+    (every year's annual means and the end state; c4_spinup pins the oracle
+    to the reference over 20 years with a decade carry)."""
+    gid = synth.land_cells()
+    ann, st, _ = _full_grid_gpu(gid, 8, 48, True, 1901, 30)
+    rng = np.random.default_rng(4)
+    sample = np.sort(rng.choice(gid.size, 64, replace=False))
+    ref = _oracle_sample(gid, sample, 8, 48, 1, 1901, 30)
+    assert ref["rc"] == 0
+    assert same_bits(ann[:, :, sample], ref["annual"])
+    got = refcase.unpack_state(st, gid.size, 8)
+    for k, v in ref["state"].items():
+        assert same_bits(got[k][sample], v), k
+
+
 @pytest.mark.parametrize("kernel", ["pair", "solo", "mixed"])
 def test_config5_l10_quarter_degree_sample(kernel, monkeypatch):
     """10 soil layers (config 5) on 0.25 deg cells, NS=24, GROW on, both
