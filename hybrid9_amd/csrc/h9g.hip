@@ -854,7 +854,11 @@ static GeoKind geo_kind(const h9g_config &c) {
 
 #if defined(H9G_ISA_ONLY)
 // tools/isa_pair.sh: device code of the config-2 pair kernel alone (ISA study)
+#if defined(H9G_ISA_L10)
+template __global__ void h9g_pair_kernel<10, GeoC<10, 24>>(const KArgs, const GeoC<10, 24>);
+#else
 template __global__ void h9g_pair_kernel<8, GeoC<8, 48>>(const KArgs, const GeoC<8, 48>);
+#endif
 #else
 static unsigned nblocks(size_t n) { return (unsigned)((n + H9G_BLOCK - 1) / H9G_BLOCK); }
 

@@ -244,16 +244,21 @@ __device__ __forceinline__ void pace_key(int &row, int &slot) {
 }
 
 // The L = 10 pair kernel runs 3 waves per SIMD like L = 8: without the
-// per-layer double reciprocals of -psi and theta_s its LDS block fits three
-// workgroups per CU (48.6 KB), and 168 VGPRs (config 5: 632 -> 535 ms per
-// year against 2 waves/SIMD with the reciprocals).
+// per-layer double reciprocal of theta_s and the day constants' its LDS block
+// fits three workgroups per CU (72 rows, 51.4 KB), and 168 VGPRs (config 5:
+// 632 -> 535 ms per year against 2 waves/SIMD with every reciprocal,
+// DESIGN.md §6).
 template <int L>
 constexpr int pair_resident() { return 3; }   // waves per SIMD (h9g.hip pair_waves)
 
 template <int L, int S>
 struct PairStore {
   static constexpr int NT = L / 2;
-  static constexpr bool kRecip = L <= 8, kRts = kRecip, kDayRecip = true;
+  // LDS fields by layer count (3 workgroups per CU: at most 75 rows).  L = 8:
+  // every reciprocal (75 rows).  L = 10 (5 rows per per-layer field): 1/(-psi)
+  // (~15 divisions per substep) instead of the day constants' reciprocals (~5;
+  // round 3: 533.6 -> 530.3 ms for config 5), no 1/theta_s (72 rows).
+  static constexpr bool kRecip = true, kRts = L <= 8, kDayRecip = L <= 8;
   // s_node of the conductivity phase from the stored 1/theta_s too (round 3:
   // no longer spills in the call-free kernel)
   static constexpr bool kRtsHK = kRts;

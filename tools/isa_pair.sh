@@ -7,7 +7,7 @@ set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 TAG=${1:-base}; shift || true
 mkdir -p /tmp/isa
-K=_Z15h9g_pair_kernelILi8EN3h9k4GeoCILi8ELi48EEEEv5KArgsT0_
+K=${ISA_K:-_Z15h9g_pair_kernelILi8EN3h9k4GeoCILi8ELi48EEEEv5KArgsT0_}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math \
   -fhip-fp32-correctly-rounded-divide-sqrt --cuda-device-only -S -DH9G_ISA_ONLY -DH9G_ISA_MARK "$@" \
   -o /tmp/isa/$TAG.s "$ROOT/hybrid9_amd/csrc/h9g.hip" \
