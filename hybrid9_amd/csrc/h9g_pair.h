@@ -987,28 +987,53 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     pr.mark(2);
     sp.template par_d<NT, 4, H9G_FE_HK>(hk_fast, hk_exact, outk);
   }
-  // Four single powers split over the pair (unused ones get base 1):
-  //   lane 0: temp0 of the aquifer node (:579-580), then zq(L+1) (:581-590);
-  //   lane 1: the specific-yield power of layer L (:937-940), then smp1 of
-  //           the aquifer row (:737-741).
-  // The aquifer node's powers and row (:574-590, :737-741, :937-940) are read
-  // only by lanes whose water table is below the column: a wave with none
-  // skips them (wave-uniform); the deepening loop's rare fall-through below
-  // the column then evaluates s_y(L) itself.
+  // First round of single powers, one per lane, chosen by where the lane's
+  // water table is (jwt = L: below the column), with the lane's operands:
+  //   below:  lane 0 temp0 of the aquifer node (:579-580), lane 1 the
+  //           specific-yield power of layer L at this zwtmm (:937-940);
+  //   inside: lane 0 the recharge conductivity's power (:874-877), lane 1
+  //           the specific-yield power of layer jwt+1 (:963-981), both of
+  //           the recharge section below, which reads only this substep's
+  //           starting theta and zwt.
+  // A wave holding columns of both kinds evaluates one round here instead of
+  // one per kind (round 3).  The second aquifer round (zq(L+1) and smp1 of the
+  // aquifer row, :581-590, :737-741) is read only by lanes below the column:
+  // a wave with none skips it (wave-uniform); the deepening loop's rare
+  // fall-through below the column evaluates s_y(L) itself for a lane inside.
   const bool any_aq = any_lane(aq);
-  FV<1> pA{{one}}, pY{{one}};
+  const int jc = aq ? L : jwt + 1;            // the layer whose -psi divides
+  float s1c = one, bsw_c = zero;              // recharge operands of layer jwt+1 (:866-873)
+  if (any_lane(!aq)) {
+    float th_j = zero;
+#pragma unroll
+    for (int i = 1; i <= L; i++)
+      if (i == jc) th_j = theta[i];
+    const float s_node = MAXX(th_j / cs.lay(PF_TS, jc), 0.01f);
+    s1c = MINC(one, s_node);
+    bsw_c = cs.lay(PF_BSW, jc);
+  }
+  FV<1> p0, p1;                               // lane 0's and lane 1's power
+  sp.template pick<1>(
+      [&](int h) __attribute__((always_inline)) -> FV<1> {
+        const float npsi = -cs.lay(PF_PSI, jc);
+        const float num = (aq && h == 0) ? (-PSI(L) + zwtmm - g.zi(L)) : zwtmm;
+        bool sq = false, sw = false;
+        float q = divr_d<CS::kRecip>(m, num, npsi, [&]() { return lay_d(cs, PF_RPSI0, jc); }, sq);
+        const float ninv = cs.lay(PF_NINVB, jc);
+        const float e = h ? ninv : (aq ? one + ninv : 2.0f * bsw_c + 3.0f);
+        float w = m.powf_d(h ? one + q : (aq ? q : s1c), e, sw);
+        if (__builtin_expect(sq | sw, 0)) {                  // one deferred check
+          H9G_BR(BR_RECH);
+          divr_fix<CS::kRecip>(m, q, num, npsi);
+          w = m.powf(h ? one + q : (aq ? q : s1c), e);
+        }
+        return FV<1>{{w}};
+      },
+      p0, p1);
+  const FV<1> pA = p0, pY = p1;
   FV<2> eA{{zero, zero}}, eS{{zero, zero}};
   if (any_aq) {
   H9G_BR(BR_ANYAQ);
-  sp.template pick<1>(
-      [&](int h) __attribute__((always_inline)) -> FV<1> {
-        const float npsi = -PSI(L);
-        const float num = sel(h, aq ? (-PSI(L) + zwtmm - g.zi(L)) : npsi, zwtmm);
-        const float q = divr<CS::kRecip>(m, num, npsi, [&]() { return lay_d(cs, PF_RPSI0, L); });
-        const float ninv = LAYF(PF_NINVB, L);
-        return FV<1>{{m.powf(sel(h, q, one + q), sel(h, one + ninv, ninv))}};
-      },
-      pA, pY);
   {
     const float d0 = aq ? (zwtmm - g.zi(L)) : one;
     float ve = LAYF(PF_PTE, L) / d0 * (1.0f - pA.v[0]);
@@ -1276,36 +1301,17 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     // operands of layer jwt+1 (and jwt): the parameters by runtime-indexed
     // store reads, the register arrays by selects
     const int j1 = jwt + 1;
-    const float ts_j = cs.lay(PF_TS, j1), hks_j = cs.lay(PF_HKS, j1), bsw_j = cs.lay(PF_BSW, j1);
-    float th_j = zero, smp_m = zero, zq_m = zero, zc_j = zero;
+    const float hks_j = cs.lay(PF_HKS, j1);
+    float smp_m = zero, zq_m = zero, zc_j = zero;
 #pragma unroll
     for (int i = 1; i <= L; i++) {
-      if (i == j1) th_j = theta[i];
       if (i == (jwt > 1 ? jwt : 1)) { smp_m = smp[i]; zq_m = zq[i]; }
       if (i == jwt) zc_j = g.zc(i);
     }
     const float wh_zwt = zero;
-    const float s_node = MAXX(th_j / ts_j, 0.01f);
-    const float s1 = MINC(one, s_node);
-    FV<1> pK, pS;
-    sp.template pick<1>(
-        [&](int h) __attribute__((always_inline)) -> FV<1> {
-          const int j1 = jwt + 1;
-          const float nb = -cs.lay(PF_PSI, j1);
-          bool sq = false, sw = false;
-          float q = divr_d<CS::kRecip>(m, zwtmm, nb, [&]() { return lay_d(cs, PF_RPSI0, j1); }, sq);
-          const float e = sel(h, 2.0f * bsw_j + 3.0f, cs.lay(PF_NINVB, j1));
-          float w = m.powf_d(h ? one + q : s1, e, sw);
-          if (__builtin_expect((h && sq) | sw, 0)) {          // one deferred check
-            H9G_BR(BR_RECH);
-            divr_fix<CS::kRecip>(m, q, zwtmm, nb);
-            w = m.powf(h ? one + q : s1, e);
-          }
-          return FV<1>{{w}};
-        },
-        pK, pS);
-    sy_first = s_y_of(jwt + 1, pS.v[0]);
-    const float ka = hks_j * pK.v[0];
+    // the two powers came from the first round above (p0, p1)
+    sy_first = s_y_of(jwt + 1, p1.v[0]);
+    const float ka = hks_j * p0.v[0];
     const float smp1m = MAXC(smpmin, smp_m);
     const float wh = smp1m - zq_m;
     if (jwt == 0)
@@ -1353,7 +1359,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
         return i != L;
       });
       if (qcharge_tot > zero) {
-        if (!any_aq) rous = s_y_at(L, zwtmm);    // pY was skipped: the same expression
+        if (!aq) rous = s_y_at(L, zwtmm);    // this lane's first round was the recharge's
         s.zwt = s.zwt - m.div(qcharge_tot, 1000.0f, r1000) / rous;
       }
     }
