@@ -720,25 +720,33 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
   // :269-276 (previous-step smp)
   float beta = zero;
   {
-    float qb[L + 1];
-    bool badb = false;
-#pragma unroll
-    for (int i = 1; i <= L; i++) {
-      qb[i] = m.div_d(smp[i] - g.zc(i), -150000.0f, 1.0 / -150000.0);
-      badb |= m.div_bad(qb[i]);
-    }
-    if (__builtin_expect(badb, 0)) {
-      H9G_BR(BR_QB);
-#pragma unroll
-      for (int i = 1; i <= L; i++) m.div_fix(qb[i], smp[i] - g.zc(i), -150000.0f);
-    }
-#pragma unroll
-    for (int i = 1; i <= L; i++) {
-      float b = one - qb[i];
+    // the terms rootr(i) * beta_i of the lane's own layers (the pair split:
+    // round 3, 199.3 -> 197.3 ms), then the reference's sum over the layers
+    // in order
+    float rb[L + 1];
+    float *const out[1] = {rb};
+    auto qb_x = [&](int t, int h) __attribute__((always_inline)) {
+      return sel(h, smp[2 * t + 1] - g.zc(2 * t + 1), smp[2 * t + 2] - g.zc(2 * t + 2));
+    };
+    auto term = [&](int t, int h, float q) __attribute__((always_inline)) {
+      float b = one - q;
       b = MINC(one, b);
       b = MAXF(zero, b);
-      beta = beta + ROOT(i) * b;
-    }
+      return FV<1>{{sp.own(cs, PF_ROOTR, t, h) * b}};
+    };
+    sp.template par_d<NT, 1, NT>(
+        [&](int t, int h, bool &bad) __attribute__((always_inline)) -> FV<1> {
+          const float q = m.div_d(qb_x(t, h), -150000.0f, 1.0 / -150000.0);
+          bad |= m.div_bad(q);
+          return term(t, h, q);
+        },
+        [&](int t, int h) __attribute__((always_inline)) -> FV<1> {
+          H9G_BR(BR_QB);
+          return term(t, h, m.div(qb_x(t, h), -150000.0f, 1.0 / -150000.0));
+        },
+        out);
+#pragma unroll
+    for (int i = 1; i <= L; i++) beta = beta + rb[i];
   }
   // :283-295
   float rsc;
