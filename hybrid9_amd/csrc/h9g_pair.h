@@ -968,7 +968,18 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
           const float thp = sel(h, theta[i0 + 1], theta[ip1]);
           const float ts = OWN(PF_TS);
           const float tsp = sel(h, TS(i0 + 1), TS(ip1));
-          float s1 = 0.5f * (th + thp) / (0.5f * (ts + tsp));
+          // s1 = RN(0.5a / 0.5b) = RN(a / b) (the halvings are exact for
+          // normal a, b), from y = PF_ITS = RN(1/b) by Markstein's correction:
+          // q0 = RN(a y), e = a - b q0 (exact), RN(q0 + e y) = RN(a / b) when
+          // nothing under- or overflows.  a, b in [2^-60, 2^60) keeps q and e
+          // normal; other operands flag the slot for hk_exact.  (The IEEE
+          // division took 11 VALU in a chain of 9; tools/markstein_check.c.)
+          const float sa = th + thp, sb = ts + tsp, its = OWN(PF_ITS);
+          const float q0 = sa * its;
+          float s1 = __builtin_fmaf(__builtin_fmaf(-sb, q0, sa), its, q0);
+          const uint32_t ua = __builtin_bit_cast(uint32_t, sa) - 0x21800000u;   // 2^-60
+          const uint32_t ub = __builtin_bit_cast(uint32_t, sb) - 0x21800000u;
+          bad |= (ua > ub ? ua : ub) >= 0x5d800000u - 0x21800000u;             // 2^60
           s1 = MINC(one, s1);
           const float bsw = OWN(PF_BSW);
           float s_node = MAXX(divr_d<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }, bad),

@@ -146,3 +146,18 @@ def test_device_fast_division_defers_on_zero_inf_nan_divisors():
     assert flag.all()
     with np.errstate(all="ignore"):
         assert same_bits(out, x / d)
+
+
+def test_markstein_quotient_of_conductivity_phase(tmp_path):
+    """hk_fast (h9g_pair.h) computes s1 = 0.5a / 0.5b (HYDROLOGY.f90:605-608)
+    from the stored RN(1/b) with one Markstein correction; it must equal the
+    IEEE quotient over the operand range it accepts (tools/markstein_check.c:
+    every b significand, midpoint-adjacent a, random a and b in [2^-60, 2^60),
+    and a control with a one-ulp-off reciprocal that must fail)."""
+    from pathlib import Path
+    src = Path(__file__).resolve().parents[1] / "tools" / "markstein_check.c"
+    exe = tmp_path / "markstein_check"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(src), "-lm"], check=True)
+    r = subprocess.run([str(exe), "8"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(": 0 mismatches") == 2, r.stdout
