@@ -1027,7 +1027,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
 #pragma unroll
     for (int i = 1; i <= L; i++)
       if (i == jc) th_j = theta[i];
-    const float s_node = MAXX(th_j / cs.lay(PF_TS, jc), 0.01f);
+    const float s_node =
+        MAXX(divr<CS::kRts>(m, th_j, cs.lay(PF_TS, jc), [&]() { return lay_d(cs, PF_RTS0, jc); }), 0.01f);
     s1c = MINC(one, s_node);
     bsw_c = cs.lay(PF_BSW, jc);
   }
