@@ -276,6 +276,56 @@ class HostFed:
         self.bufs = []
 
 
+class NcFed:
+    """--forcing nc4: the config-3 "async PGF prefetch" path from files.
+    Synthetic PGF netCDF-4 files of one year (0.5 deg, per-day chunks,
+    shuffle + deflate, tools/pgf_synth.py) are written before the timed
+    region; every step reads its year's days from them with
+    h9g_nc_forcing_prefetch (host thread pool: direct chunk reads, inflate,
+    gather; then an async copy into the slot) into one of two slots, the next
+    year's read overlapping the current kernel.  The first read of the timed
+    region is not overlapped.  Every year reads the same file year (its
+    days 0..nday-1), so only year 1 matches the device-generated run."""
+
+    def __init__(self, ctx, W, directory):
+        sys.path.insert(0, str(ROOT / "tools"))
+        import pgf_synth
+        import hybrid9_amd as h
+        self.ctx, self.W = ctx, W
+        t = time.perf_counter()
+        self.paths = pgf_synth.write_year(directory, 1901, 366)
+        self.write_s = time.perf_counter() - t
+        self.bytes = sum(os.path.getsize(p) for p in self.paths)
+        self.k = 0
+        self.nx, self.ny = 720, 360
+        # a synchronous read of one year, for the ingest rate alone
+        g = np.asarray(ctx._gid if hasattr(ctx, "_gid") else [], np.int64)
+        self.read_s = None
+        if g.size:
+            t = time.perf_counter()
+            h.nc_forcing_read(self.paths, self.nx, self.ny, g, 0, 365)
+            self.read_s = time.perf_counter() - t
+
+    def step(self, s):
+        from hybrid9_amd import synth
+        y, slot = 1901 + s, self.k % 2
+        nd = synth.days_in_year(y)
+        if self.k == 0 or self.k == self.W:
+            self.ctx.nc_prefetch(slot, self.paths, self.nx, self.ny, 0, nd)
+        self.ctx.run_year(slot, y)                       # joins this slot's read first
+        if self.k + 1 != self.W:
+            self.ctx.nc_prefetch(1 - slot, self.paths, self.nx, self.ny, 0, synth.days_in_year(y + 1))
+        self.k += 1
+
+    def describe(self):
+        import hybrid9_amd as h
+        return {"source": "synthetic PGF v2.1 netCDF-4 files (one chunk per day, shuffle + deflate 4)",
+                "file_bytes_per_year": int(self.bytes), "write_s": self.write_s,
+                "read_s_per_year_sync": self.read_s,
+                "io_threads": int(os.environ.get("H9G_IO_THREADS", "0")) or min(16, os.cpu_count() or 1),
+                "slots": 2, "reader": "h9g_nc_forcing_prefetch (direct chunk reads, libdeflate, host pool)"}
+
+
 def plan(workload: str, W: int, K: int, world: int = 1, rank: int = 0, strong: bool = False,
          seed: int | None = None) -> dict:
     """Everything a rank's run is made of, decided on the host (no GPU):
@@ -385,7 +435,12 @@ def main():
     ap.add_argument("--host-fed", action="store_true",
                     help="PCIe-inclusive rate: every step's forcing year is copied from pinned host "
                          "memory (async, double-buffered); reported in DESIGN.md, never as `value`")
+    ap.add_argument("--forcing", choices=["device", "nc4"], default="device",
+                    help="nc4: every step's forcing is read from synthetic PGF netCDF-4 files through "
+                         "h9g_nc_forcing_prefetch (ingest-inclusive; DESIGN.md, never as `value`)")
     args = ap.parse_args()
+    if args.forcing == "nc4" and (args.host_fed or WORKLOADS[args.workload]["grid"] != "05"):
+        raise SystemExit("--forcing nc4: 0.5 deg workloads only, not with --host-fed")
     wl = WORKLOADS[args.workload]
     K = args.steps if args.steps is not None else wl.get("steps", 3)
     W = args.warmup if args.warmup is not None else wl.get("warmup", 1)
@@ -409,14 +464,22 @@ def main():
     nslots = pl["nslots"]
     if args.host_fed:
         nslots = max(2, min(4, W + K))            # 2 push slots + up to 4 source years
+    if args.forcing == "nc4":
+        nslots = 2
     ctx = h.Context(gid.size, pl["zi"], nlayers=L, nisurf=ns, grow_on=wl["grow_on"],
                     nslots=nslots, device=local if world > 1 else 0)
     ctx.set_cells(gid, lat)
     ctx.synth_params(seed)
     ctx.init_state()
     src_years = pl["slot_year"] if not args.host_fed else years[:nslots]
-    for slot, y in enumerate(src_years):           # forcing resident in HBM
-        ctx.synth_forcing(slot, seed, synth.year_day0(y), synth.days_in_year(y))
+    nc_fed = None
+    if args.forcing == "nc4":
+        ctx._gid = gid
+        nc_fed = NcFed(ctx, W, tempfile.mkdtemp(prefix="h9pgf_"))
+        pl = dict(pl, slot_of_step=[None] * (W + K))
+    else:
+        for slot, y in enumerate(src_years):       # forcing resident in HBM
+            ctx.synth_forcing(slot, seed, synth.year_day0(y), synth.days_in_year(y))
     ctx.sync()
 
     if args.host_fed:
@@ -436,10 +499,15 @@ def main():
         def total_kernel_ms(self, reset=False):
             return self.c.total_kernel_ms(reset)
 
+    class _NcFed(_Fed):                              # --forcing nc4: read, then run
+        def run_year(self, _slot, y):
+            nc_fed.step(y - 1901)
+
     def sync():
         barrier_sync(ctx, torch, dist, world)
 
-    elapsed = timed_steps(_Fed(ctx) if host_fed else ctx, pl, exchange, sync)
+    runner = _Fed(ctx) if host_fed else (_NcFed(ctx) if nc_fed else ctx)
+    elapsed = timed_steps(runner, pl, exchange, sync)
     kern_ms = ctx.total_kernel_ms(reset=True)
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
@@ -502,8 +570,12 @@ def main():
     if host_fed is not None:
         out["host_fed"] = host_fed.describe()
         host_fed.close()
+    if nc_fed is not None:
+        out["forcing"] = nc_fed.describe()
+        out["data"] = "synthetic forcing read from netCDF-4 files each step (tools/pgf_synth.py)"
+        subprocess.run(["rm", "-rf", str(Path(nc_fed.paths[0]).parent)])
     ctx.close()
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and host_fed is None:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and host_fed is None and nc_fed is None:
         out["cpu_baseline"] = cpu_baseline(wl, synth.SEED)
     if world > 1:
         dist.barrier()

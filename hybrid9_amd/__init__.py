@@ -36,6 +36,7 @@ STOP_MESSAGES = {  # HYDROLOGY.f90 STOP sites
     2: "Problem with tridiagonal 2.",            # :818-825
     3: "rsub_top_tot is positive in drainage",   # :1068-1072
     4: "Problem in HYDROLOGY: Water imbalance > 0.1 mm",  # :1244-1274
+    5: "internal: exact re-run requested with no day snapshot",   # H9G_ERR_NOSNAP (not a reference STOP)
 }
 LMAX = 10
 MAX_SLOTS = 512          # H9G_MAX_SLOTS

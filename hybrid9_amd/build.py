@@ -19,7 +19,7 @@ SRC = HERE / "csrc" / "h9g.hip"
 SRC_IO = HERE / "csrc" / "h9g_io.cpp"       # host-only NetCDF I/O
 DEPS = [SRC, SRC_IO, HERE / "csrc" / "h9_math.h", HERE / "csrc" / "h9g_step.h",
         HERE / "csrc" / "h9g_synth.h", HERE / "csrc" / "h9g_geo.h",
-        HERE / "csrc" / "h9g_pair.h",
+        HERE / "csrc" / "h9g_pair.h", HERE / "csrc" / "h9g_io.h",
         HERE.parent / "include" / "h9g.h"]
 OUT = HERE / "lib" / "libh9g.so"
 ARCH = os.environ.get("H9G_ARCH", "gfx950")
@@ -60,18 +60,43 @@ def up_to_date() -> bool:
     return all(d.stat().st_mtime <= t for d in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False, extra=()) -> Path:
-    if not force and up_to_date():
-        return OUT
-    OUT.parent.mkdir(parents=True, exist_ok=True)
-    tmp = OUT.with_suffix(".so.tmp")
-    cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, *extra, id_flag(extra), str(SRC), str(SRC_IO), "-o",
-           str(tmp)]
+def _run(cmd, verbose):
     if verbose:
         print(" ".join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed:\n{r.stderr[-4000:]}")
+
+
+def build(force: bool = False, verbose: bool = False, extra=()) -> Path:
+    """Compiles the two translation units to objects (the device code, ~4
+    minutes, and the host-only NetCDF I/O, seconds; each only when its own
+    inputs changed, keyed by their digest) and links libh9g.so."""
+    if not force and up_to_date():
+        return OUT
+    OUT.parent.mkdir(parents=True, exist_ok=True)
+    obj = OUT.parent / "obj"
+    obj.mkdir(exist_ok=True)
+    import hashlib
+    flags = [f"--offload-arch={ARCH}", *FLAGS, *extra]
+    objs = []
+    # h9g_build_id lives in the I/O unit: only it gets the digest flag
+    for src, deps, idf in ((SRC, [d for d in DEPS if d != SRC_IO], []),
+                           (SRC_IO, [SRC_IO, HERE / "csrc" / "h9g_io.h", DEPS[-1]], [id_flag(extra)])):
+        flags_u = flags + idf
+        hs = hashlib.sha256(" ".join(flags_u).encode())
+        for d in deps:
+            hs.update(d.read_bytes())
+        o = obj / f"{src.stem}_{hs.hexdigest()[:16]}.o"
+        if force or not o.exists():
+            for old in obj.glob(f"{src.stem}_*.o"):
+                old.unlink()
+            tmp = o.with_suffix(".o.tmp")
+            _run([hipcc(), *[f for f in flags_u if f != "-shared"], "-c", str(src), "-o", str(tmp)], verbose)
+            os.replace(tmp, o)
+        objs.append(str(o))
+    tmp = OUT.with_suffix(".so.tmp")
+    _run([hipcc(), f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-o", str(tmp)], verbose)
     os.replace(tmp, OUT)
     return OUT
 

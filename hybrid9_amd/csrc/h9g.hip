@@ -34,6 +34,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -43,8 +45,10 @@
 #include "h9g_step.h"
 #include "h9g_pair.h"
 #include "h9g_synth.h"
+#include "h9g_io.h"
 
 using namespace h9k;
+static_assert(H9G_ERR_NOSNAP_K == H9G_ERR_NOSNAP, "kernel and ABI error codes");
 
 __constant__ uint64_t c_exp2tab[32] = H9M_EXP2F_TAB_INIT;
 __constant__ double c_log2tab[32] = H9M_POWF_LOG2_TAB_INIT;
@@ -79,6 +83,7 @@ struct KArgs {
   unsigned *__restrict__ stamps;   // H9G_STAMPS builds: 8 phase cycle sums per wave
   float *__restrict__ sv;          // pair kernel: day snapshot, PairStore::GBLOCK bytes per workgroup
   const int *__restrict__ perm;    // lane slot -> cell (h9g_sort_kernel), or null: identity
+  int sorted_io;                   // 1: forc and annual are in slot order (h9g_perm_forcing_kernel; round 4)
   int *__restrict__ hist;          // per cell: substeps of the year with the water table below the column
   unsigned *__restrict__ pace;     // pair kernel, Pacer mode 2: H9G_PACE_ROWS x 16 progress words
   unsigned epoch;                  // Pacer mode 2: launch tag
@@ -133,6 +138,7 @@ h9g_pair_kernel(const KArgs a, const G g) {
   const int slot = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * H9G_PCPW + (lane >> 1);
   if (slot >= a.cend) return;        // both lanes of a pair leave together
   const int c = a.perm ? a.perm[slot] : slot;
+  const int io = a.sorted_io ? slot : c;   // forcing and annual sums: slot order when sorted
   const int n = a.ncell;
 
   int prow, pslot;
@@ -173,7 +179,7 @@ h9g_pair_kernel(const KArgs a, const G g) {
   if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
     if (h == 0)
 #pragma unroll
-      for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + c] = __builtin_nanf("");
+      for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + io] = __builtin_nanf("");
     return;
   }
   cell_inv_pair<L, G>(g, cs);
@@ -181,18 +187,19 @@ h9g_pair_kernel(const KArgs a, const G g) {
   float errval = 0.0f;
 #if defined(H9G_STAMPS)
   StampProf pr{stamp_clock(), {0, 0, 0, 0, 0, 0, 0, 0}};
-  const int code = cell_year_pair<L, G, Split2, PS, true>(g, cs, sp, s, (const gbl_float *)(a.forc + c), (size_t)n, a.fvar, a.nt,
-                                                         a.nisurf, a.grow_on, (gbl_float *)(a.annual + c), (size_t)n, eday,
+  const int code = cell_year_pair<L, G, Split2, PS, true>(g, cs, sp, s, (const gbl_float *)(a.forc + io), (size_t)n, a.fvar, a.nt,
+                                                         a.nisurf, a.grow_on, (gbl_float *)(a.annual + io), (size_t)n, eday,
                                                          estep, errval, T, pr);
   if (lane == 0 && a.stamps)
     for (int k = 0; k < 8; k++) a.stamps[(blockIdx.x * H9G_PWAVES + wave) * 8 + k] = pr.acc[k];
 #else
-  const int code = cell_year_pair<L, G>(g, cs, sp, s, (const gbl_float *)(a.forc + c), (size_t)n, a.fvar, a.nt, a.nisurf,
-                                        a.grow_on, (gbl_float *)(a.annual + c), (size_t)n, eday, estep, errval, T);
+  const int code = cell_year_pair<L, G>(g, cs, sp, s, (const gbl_float *)(a.forc + io), (size_t)n, a.fvar, a.nt, a.nisurf,
+                                        a.grow_on, (gbl_float *)(a.annual + io), (size_t)n, eday, estep, errval, T);
 #endif
   if (h != 0) return;                // the even lane writes the cell back
-  int cw = c;
+  int cw = c, iow = io;
   opaque(cw);
+  opaque(iow);
   cs.launder();
   if (a.hist) a.hist[cw] = s.naq;
   const size_t ow = (size_t)(4 * L + 1) * n + cw;
@@ -218,7 +225,7 @@ h9g_pair_kernel(const KArgs a, const G g) {
     a.err[3 * (size_t)n + cw] = __builtin_bit_cast(int, errval);
     atomicOr(a.err_flag, 1);
 #pragma unroll
-    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + cw] = __builtin_nanf("");
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + iow] = __builtin_nanf("");
   }
 }
 
@@ -239,6 +246,7 @@ h9g_solo_kernel(const KArgs a, const G g) {
   const int slot = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x);
   if (slot >= a.cend) return;
   const int c = a.perm ? a.perm[slot] : slot;
+  const int io = a.sorted_io ? slot : c;
   const int n = a.ncell;
   SS cs{(lds_float *)&s_cell[threadIdx.x], (const lds_float *)s_zt};
   const SplitAll sp;
@@ -269,17 +277,18 @@ h9g_solo_kernel(const KArgs a, const G g) {
   for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.lay(PF_TS, i);
   if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
 #pragma unroll
-    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + c] = __builtin_nanf("");
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + io] = __builtin_nanf("");
     return;
   }
   cell_inv_pair<L, G>(g, cs);
   int eday = 0, estep = 0;
   float errval = 0.0f;
-  const int code = cell_year_pair<L, G, SplitAll, SS, false>(g, cs, sp, s, (const gbl_float *)(a.forc + c), (size_t)n, a.fvar,
-                                                             a.nt, a.nisurf, a.grow_on, (gbl_float *)(a.annual + c),
+  const int code = cell_year_pair<L, G, SplitAll, SS, false>(g, cs, sp, s, (const gbl_float *)(a.forc + io), (size_t)n, a.fvar,
+                                                             a.nt, a.nisurf, a.grow_on, (gbl_float *)(a.annual + io),
                                                              (size_t)n, eday, estep, errval, T);
-  int cw = c;
+  int cw = c, iow = io;
   opaque(cw);
+  opaque(iow);
   cs.launder();
   if (a.hist) a.hist[cw] = s.naq;
   const size_t ow = (size_t)(4 * L + 1) * n + cw;
@@ -305,8 +314,51 @@ h9g_solo_kernel(const KArgs a, const G g) {
     a.err[3 * (size_t)n + cw] = __builtin_bit_cast(int, errval);
     atomicOr(a.err_flag, 1);
 #pragma unroll
-    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + cw] = __builtin_nanf("");
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + iow] = __builtin_nanf("");
   }
+}
+
+// The year's forcing in the year kernel's slot order (round 4, VERDICT r03
+// #5): dst[v][d][s] = src[v][d][perm[s]].  With the cells re-ordered each
+// year (h9g_sort_kernel), a wave's daily forcing loads by cell id scattered
+// over its XCD's range, so the non-temporal loads of neighbouring lanes hit
+// different lines: 4.45 GB fetched per config-2 launch for 0.69 GB of
+// forcing (pmc_r03i.json).  One gather per year makes every wave's daily
+// loads contiguous again.  XCD-aware like the year kernel: the launch range
+// [c0, cend) is cut into the year kernel's workgroups of cpb slots, dealt to
+// the XCDs as xcd_vwg deals them, and block L (XCD L % 8) copies PF_ROWS
+// rows of one workgroup of XCD L % 8 -- so it reads only cells of its own
+// XCD's range, which the sort never leaves.
+#define H9G_PF_ROWS 32
+__global__ void __launch_bounds__(256) h9g_perm_forcing_kernel(int c0, int cend, int cpb, int nt, int n, size_t fvar,
+                                                               const int *__restrict__ perm,
+                                                               const float *__restrict__ src, float *__restrict__ dst) {
+  const unsigned nb = (unsigned)((cend - c0 + cpb - 1) / cpb), x = blockIdx.x % H9G_NXCD, j = blockIdx.x / H9G_NXCD;
+  const unsigned q = nb / H9G_NXCD, r = nb % H9G_NXCD, cnt = q + (x < r ? 1u : 0u);
+  const unsigned rows = 7u * (unsigned)nt, rgroups = (rows + H9G_PF_ROWS - 1) / H9G_PF_ROWS;
+  if (cnt == 0 || j >= cnt * rgroups) return;
+  const unsigned v = x * q + (x < r ? x : r) + j % cnt, r0 = (j / cnt) * H9G_PF_ROWS;
+  for (unsigned t = threadIdx.x; t < (unsigned)cpb * H9G_PF_ROWS; t += blockDim.x) {
+    const int s = c0 + (int)(v * (unsigned)cpb + t % (unsigned)cpb);
+    const unsigned row = r0 + t / (unsigned)cpb;
+    if (s >= cend || row >= rows) continue;
+    const size_t off = (size_t)(row / (unsigned)nt) * fvar + (size_t)(row % (unsigned)nt) * n;
+    dst[off + s] = src[off + perm[s]];
+  }
+}
+static unsigned perm_forcing_blocks(int c0, int cend, int cpb, int nt) {
+  const unsigned nb = (unsigned)((cend - c0 + cpb - 1) / cpb);
+  const unsigned cmax = nb / H9G_NXCD + (nb % H9G_NXCD ? 1u : 0u);
+  return H9G_NXCD * cmax * ((7u * (unsigned)nt + H9G_PF_ROWS - 1) / H9G_PF_ROWS);
+}
+
+// The annual sums of a sorted year kernel (slot order) back to cell order.
+__global__ void __launch_bounds__(256) h9g_unperm_annual_kernel(int n, int rows, const int *__restrict__ perm,
+                                                                const float *__restrict__ src, float *__restrict__ dst) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const int c = perm[s];
+  for (int r = blockIdx.y; r < rows; r += gridDim.y) dst[(size_t)r * n + c] = src[(size_t)r * n + s];
 }
 
 // Cell order of the next year kernel: a stable counting sort of the cells
@@ -786,6 +838,8 @@ struct h9g_ctx {
   int *d_slow = nullptr;
   float *d_sv = nullptr;          // pair kernel day-snapshot blocks
   int *d_perm = nullptr;          // cell order of the year kernel (h9g_sort_kernel)
+  float *d_forc_s = nullptr;      // the year's forcing in slot order (h9g_perm_forcing_kernel)
+  float *d_ann_s = nullptr;       // the year kernel's annual sums in slot order
   unsigned *d_aqbits = nullptr;   // H9G_DUMP_AQ builds: day-level water-table record of the last year
   int *d_hist = nullptr;          // per cell: substeps of the last year below the column (-1: none)
   int hist_nsub = 0;              // substeps of that year
@@ -830,6 +884,19 @@ static GeoKind geo_kind(const h9g_config &c) {
 }
 
 // Launch a templated kernel K<L, G> with the context's geometry variant.
+#if defined(H9G_ONLY_C2)
+// A/B measurement builds (tools/build_variant.py --c2): the driver's config-2
+// instantiation only (L = 8, driver.txt layers, NISURF = 48), ~1 minute
+// instead of ~4 to build; any other configuration is refused.
+#define H9G_DISPATCH(ctx, KERNEL, GRID, BLOCK, STREAM, ...)                          \
+  do {                                                                               \
+    if ((ctx)->L != 8 || geo_kind((ctx)->cfg) != GEO_C48) {                          \
+      fprintf(stderr, "h9g: H9G_ONLY_C2 build runs config 2 only\n");                \
+      return H9G_EINVAL;                                                             \
+    }                                                                                \
+    KERNEL<8, GeoC<8, 48>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__, GeoC<8, 48>());  \
+  } while (0)
+#else
 #define H9G_DISPATCH(ctx, KERNEL, GRID, BLOCK, STREAM, ...)                          \
   do {                                                                               \
     const GeoKind gk_ = geo_kind((ctx)->cfg);                                        \
@@ -851,6 +918,7 @@ static GeoKind geo_kind(const h9g_config &c) {
                                                          make_geo_r<10>((ctx)->cfg.zi, (ctx)->cfg.nisurf)); \
     }                                                                                \
   } while (0)
+#endif
 
 #if defined(H9G_ISA_ONLY)
 // tools/isa_pair.sh: device code of the config-2 pair kernel alone (ISA study)
@@ -894,6 +962,8 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_stamps);
   (void)hipFree(ctx->d_slow);
   (void)hipFree(ctx->d_perm);
+  (void)hipFree(ctx->d_forc_s);
+  (void)hipFree(ctx->d_ann_s);
   (void)hipFree(ctx->d_hist);
   (void)hipFree(ctx->d_aqbits);
   (void)hipFree(ctx->d_pace);
@@ -938,8 +1008,10 @@ size_t h9g_config_bytes(const h9g_config *cfg) {
   if (!cfg || cfg->ncell <= 0 || cfg->nlayers < 1 || cfg->max_days < 1 || cfg->nslots < 1) return 0;
   const size_t n = (size_t)cfg->ncell, L = (size_t)cfg->nlayers;
   const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
-  return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * (size_t)cfg->nslots +
-                          (12 + L) + 1) * n +
+  // + the slot-ordered copies of a forcing slot and of the annual sums
+  // (h9g_run_year, allocated on first use)
+  return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * ((size_t)cfg->nslots + 1) +
+                          2 * (12 + L) + 1) * n +
          sizeof(int) * 7 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
          ((n + per_block - 1) / per_block) * PairStore<8, H9G_PLANES>::GBLOCK +
          sizeof(unsigned) * 16 * (size_t)H9G_PACE_ROWS;
@@ -1269,6 +1341,7 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   a.stamps = nullptr;
   a.sv = nullptr;
   a.perm = nullptr;
+  a.sorted_io = 0;
   a.hist = ctx->d_hist;
   if (ctx->sort) {             // per launch range and its workgroup size (h9g_sort_kernel)
     const int n = (int)ctx->n, ns = (int)ctx->n_solo, pcpb = H9G_PCPW * H9G_PWAVES;
@@ -1288,6 +1361,28 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
     }
     HIPCHK(hipGetLastError());
     a.perm = ctx->d_perm;
+#if !defined(H9G_DUMP_AQ)                 // (that record is indexed by the annual array's cell)
+    // forcing and annual sums in slot order for the year kernel
+    if (!ctx->d_forc_s) HIPCHK(hipMalloc(&ctx->d_forc_s, sizeof(float) * 7 * (size_t)ctx->cfg.max_days * ctx->n));
+    if (!ctx->d_ann_s) HIPCHK(hipMalloc(&ctx->d_ann_s, sizeof(float) * (12 + ctx->L) * ctx->n));
+    // per launch range with its workgroup size, as the sort above
+    auto perm_range = [&](int c0, int cend, int cpb) {
+      h9g_perm_forcing_kernel<<<perm_forcing_blocks(c0, cend, cpb, nt), 256, 0, ctx->sc>>>(
+          c0, cend, cpb, nt, n, a.fvar, ctx->d_perm, a.forc, ctx->d_forc_s);
+    };
+    if (ctx->kind == 2) {
+      perm_range(0, n, H9G_YBLOCK);
+    } else if (ctx->kind == 3) {
+      if (ns > 0) perm_range(0, ns, H9G_YBLOCK);
+      if (ns < n) perm_range(ns, n, pcpb);
+    } else {
+      perm_range(0, n, pcpb);
+    }
+    HIPCHK(hipGetLastError());
+    a.forc = ctx->d_forc_s;
+    a.annual = ctx->d_ann_s;
+    a.sorted_io = 1;
+#endif
   }
   if (ctx->kind != 2) {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
@@ -1376,6 +1471,11 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1[e], ctx->sc));
   HIPCHK(hipEventRecord(ctx->ev_consumed[slot], ctx->sc));
+  if (a.sorted_io) {
+    h9g_unperm_annual_kernel<<<dim3((unsigned)((ctx->n + 255) / 256), (unsigned)(12 + ctx->L)), 256, 0, ctx->sc>>>(
+        (int)ctx->n, 12 + ctx->L, ctx->d_perm, ctx->d_ann_s, ctx->d_ann);
+    HIPCHK(hipGetLastError());
+  }
   h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)ctx->n, ctx->L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
   HIPCHK(hipGetLastError());
   ctx->last_year = jyear;
@@ -1643,9 +1743,11 @@ int h9g_synth_forcing(h9g_ctx *ctx, int slot, uint64_t seed, int day0, int nday)
 
 // Async PGF prefetch (READ_PGF.f90 on a host thread): days [t0, t0+nt) of
 // the 7 NetCDF files are gathered for the context's cells (h9g_set_cells)
-// into the slot's pinned staging buffer, then copied into the slot on the
-// copy stream.  h9g_run_year on that slot joins the thread first, so the
-// read of year y+1 overlaps the kernel of year y.
+// into the slot's pinned staging buffer by the reader's thread pool, and
+// copied into the slot on the copy stream in 8 day groups, each as soon as
+// the pool has filled it (round 4: the copy overlaps the rest of the read
+// instead of following it).  h9g_run_year on that slot joins the thread
+// first, so the read of year y+1 overlaps the kernel of year y.
 int h9g_nc_forcing_prefetch(h9g_ctx *ctx, int slot, const char *const *paths, int nx, int ny, int t0, int nt) {
   if (!ctx || slot < 0 || slot >= ctx->cfg.nslots || !paths || nt < 1 || nt > ctx->cfg.max_days || t0 < 0)
     return H9G_EINVAL;
@@ -1664,8 +1766,26 @@ int h9g_nc_forcing_prefetch(h9g_ctx *ctx, int slot, const char *const *paths, in
   ctx->prefetch[slot] = std::thread([ctx, slot, p, nx, ny, t0, nt]() {
     const char *pp[H9G_NFORCING];
     for (int k = 0; k < H9G_NFORCING; k++) pp[k] = p[k].c_str();
-    int rc = h9g_nc_forcing_read(pp, nx, ny, (int)ctx->n, ctx->h_gid.data(), t0, nt, ctx->h_pin[slot]);
-    if (rc == 0) rc = push_impl(ctx, slot, nt, ctx->h_pin[slot], hipMemcpyHostToDevice, true);
+    if (hipSetDevice(ctx->device) != hipSuccess ||
+        hipStreamWaitEvent(ctx->sx, ctx->ev_consumed[slot], 0) != hipSuccess) {
+      ctx->prefetch_rc[slot] = H9G_EHIP;
+      return;
+    }
+    const size_t n = ctx->n;
+    float *dst = h9g_forcing_slot(ctx, slot), *src = ctx->h_pin[slot];
+    std::atomic<int> hip_rc{0};
+    std::mutex q;                      // one enqueuer at a time on the copy stream
+    int rc = h9g_nc_read_groups(pp, nx, ny, (int)n, ctx->h_gid.data(), t0, nt, src, 8, [&](int d0, int d1) {
+      std::lock_guard<std::mutex> g(q);
+      // days [d0, d1) of the 7 variables: staging (7, nt, n) -> slot (7, max_days, n)
+      if (hipSetDevice(ctx->device) != hipSuccess ||
+          hipMemcpy2DAsync(dst + (size_t)d0 * n, sizeof(float) * ctx->cfg.max_days * n, src + (size_t)d0 * n,
+                           sizeof(float) * nt * n, sizeof(float) * (size_t)(d1 - d0) * n, 7, hipMemcpyHostToDevice,
+                           ctx->sx) != hipSuccess)
+        hip_rc = H9G_EHIP;
+    });
+    if (rc == 0 && hip_rc) rc = hip_rc;
+    if (rc == 0 && hipEventRecord(ctx->ev_copied[slot], ctx->sx) != hipSuccess) rc = H9G_EHIP;
     ctx->prefetch_rc[slot] = rc;
   });
   return 0;
@@ -1768,12 +1888,8 @@ double h9g_total_kernel_ms(h9g_ctx *ctx, int reset) {
 
 const char *h9g_kernel_name(h9g_ctx *ctx) { return ctx ? ctx->kname : ""; }
 
-#ifndef H9G_BUILD_ID
-#define H9G_BUILD_ID "unknown"
-#endif
-// Digest of the sources and flags this library was compiled from
-// (hybrid9_amd/build.py build_id); profiles record it, bench.py matches it.
-const char *h9g_build_id(void) { return H9G_BUILD_ID; }
+// (h9g_build_id is defined in h9g_io.cpp, the translation unit that is
+// recompiled with every build.)
 
 int h9g_math_selftest(int device, int n, const float *x, const float *y, float *out) {
   if (n <= 0 || !x || !out) return H9G_EINVAL;

@@ -24,10 +24,15 @@
 // WRITE_NET_CDF_3DR.f90:93), readable by every netCDF tool and by
 // scipy.io.netcdf_file.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <unistd.h>
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <mutex>
 #include <type_traits>
@@ -36,6 +41,7 @@
 #include <vector>
 
 #include "../../include/h9g.h"
+#include "h9g_io.h"
 
 namespace {
 
@@ -233,6 +239,18 @@ struct H5Api {
   int (*sclose)(hid_t_);
   int (*dread)(hid_t_, hid_t_, hid_t_, hid_t_, hid_t_, void *);
   hid_t_ *native_float;
+  // chunk table of a dataset (HDF5 >= 1.10.5): the direct chunk path below
+  bool chunks = false;
+  hid_t_ (*dget_create_plist)(hid_t_);
+  int (*pget_layout)(hid_t_);
+  int (*pget_chunk)(hid_t_, int, hsize_t_ *);
+  int (*pget_nfilters)(hid_t_);
+  int (*pget_filter2)(hid_t_, unsigned, unsigned *, size_t *, unsigned *, size_t, char *, unsigned *);
+  int (*pclose)(hid_t_);
+  size_t (*tget_size)(hid_t_);
+  int (*tget_order)(hid_t_);
+  int (*dget_num_chunks)(hid_t_, hid_t_, hsize_t_ *);
+  int (*dget_chunk_info)(hid_t_, hid_t_, hsize_t_, hsize_t_ *, unsigned *, uint64_t *, hsize_t_ *);
 };
 
 const H5Api &h5() {
@@ -270,6 +288,19 @@ const H5Api &h5() {
     ok = ok && a.native_float && a.open() >= 0;
     if (ok) a.eset_auto2(0, nullptr, nullptr);     // H5E_DEFAULT: no error stack printing
     a.ok = ok;
+    if (ok) {
+      get(a.dget_create_plist, "H5Dget_create_plist");
+      get(a.pget_layout, "H5Pget_layout");
+      get(a.pget_chunk, "H5Pget_chunk");
+      get(a.pget_nfilters, "H5Pget_nfilters");
+      get(a.pget_filter2, "H5Pget_filter2");
+      get(a.pclose, "H5Pclose");
+      get(a.tget_size, "H5Tget_size");
+      get(a.tget_order, "H5Tget_order");
+      get(a.dget_num_chunks, "H5Dget_num_chunks");
+      get(a.dget_chunk_info, "H5Dget_chunk_info");
+      a.chunks = ok;
+    }
   });
   return a;
 }
@@ -324,9 +355,9 @@ struct H5Field {
       a.dclose(d);
     }
   }
-  // values of day t, (lat, lon) row-major, converted to float by HDF5
-  bool read_day(hsize_t_ t, float *out) {
-    const hsize_t_ start[3] = {t, 0, 0}, count[3] = {1, dims[1], dims[2]}, mdim[1] = {dims[1] * dims[2]};
+  // rows [y0, y0+ny) of day t, row-major, converted to float by HDF5
+  bool read_rows(hsize_t_ t, hsize_t_ y0, hsize_t_ ny, float *out) {
+    const hsize_t_ start[3] = {t, y0, 0}, count[3] = {1, ny, dims[2]}, mdim[1] = {ny * dims[2]};
     if (a.sselect_hyperslab(space, 0 /* H5S_SELECT_SET */, start, nullptr, count, nullptr) < 0) return false;
     const hid_t_ mem = a.screate_simple(1, mdim, nullptr);
     const int rc = a.dread(dset, *a.native_float, mem, space, 0, out);
@@ -359,6 +390,194 @@ long h5_ntimes(const char *path) {
     if (fld.open(path)) n = (long)fld.dims[0];
   }
   return n;
+}
+
+// ------------------------------------------- direct chunk reads (round 4)
+// The PGF netCDF-4 files are chunked, shuffled and deflated float fields.
+// Reading them day by day through H5Dread (round 3) runs every chunk's
+// inflate inside HDF5, whose global lock serialises the threads of a
+// thread-safe build (this image's 1.10.6 is one): 53 s per 0.5 deg year in
+// an 8-core container.  Instead the chunk table (file address,
+// stored size, filter mask of each chunk) is read once through HDF5, and
+// the chunks the context's cells fall in are then read with pread, inflated
+// (libdeflate, else zlib) and unshuffled on a pool of host threads outside
+// HDF5.  Any other layout (a non-float or fletcher32-checked field, a filter
+// other than shuffle/deflate) takes the H5Dread path.
+struct Inflate {
+  bool ok = false;
+  void *(*alloc)(void) = nullptr;                                        // libdeflate
+  int (*zlib)(void *, const void *, size_t, void *, size_t, size_t *) = nullptr;
+  void (*release)(void *) = nullptr;
+  int (*uncompress)(unsigned char *, unsigned long *, const unsigned char *, unsigned long) = nullptr;   // zlib
+};
+const Inflate &inflater() {
+  static Inflate z;
+  static std::once_flag once;
+  std::call_once(once, []() {
+    for (const char *lib : {"libdeflate.so.0", "/opt/conda/lib/libdeflate.so.0"})
+      if (void *h = dlopen(lib, RTLD_NOW | RTLD_LOCAL)) {
+        z.alloc = reinterpret_cast<void *(*)(void)>(dlsym(h, "libdeflate_alloc_decompressor"));
+        z.zlib = reinterpret_cast<int (*)(void *, const void *, size_t, void *, size_t, size_t *)>(
+            dlsym(h, "libdeflate_zlib_decompress"));
+        z.release = reinterpret_cast<void (*)(void *)>(dlsym(h, "libdeflate_free_decompressor"));
+        if (z.alloc && z.zlib && z.release) { z.ok = true; return; }
+        z.alloc = nullptr;
+        z.zlib = nullptr;
+        z.release = nullptr;
+      }
+    for (const char *lib : {"libz.so.1", "/opt/conda/lib/libz.so.1"})
+      if (void *h = dlopen(lib, RTLD_NOW | RTLD_LOCAL)) {
+        z.uncompress = reinterpret_cast<int (*)(unsigned char *, unsigned long *, const unsigned char *,
+                                                unsigned long)>(dlsym(h, "uncompress"));
+        if (z.uncompress) { z.ok = true; return; }
+      }
+  });
+  return z;
+}
+// zlib stream `in` -> exactly n_out bytes; st: per-thread libdeflate state
+bool inflate_exact(void *&st, const unsigned char *in, size_t n_in, unsigned char *out, size_t n_out) {
+  const Inflate &z = inflater();
+  if (z.zlib) {
+    if (!st) st = z.alloc();
+    size_t got = 0;
+    return st && z.zlib(st, in, n_in, out, n_out, &got) == 0 && got == n_out;
+  }
+  if (!z.uncompress) return false;
+  unsigned long got = n_out;
+  return z.uncompress(out, &got, in, n_in) == 0 && got == n_out;
+}
+
+struct Chunked {               // a (time, lat, lon) field stored as filtered chunks
+  hsize_t_ dims[3] = {0, 0, 0}, cd[3] = {0, 0, 0};
+  int nfilt = 0;
+  int filt[8] = {0};           // pipeline order (applied in this order on write)
+  bool be = false;
+  struct Ch {
+    hsize_t_ c[3];
+    uint64_t addr, size;
+    unsigned mask;
+  };
+  std::vector<Ch> ch;
+  // true if the field's chunks can be read and decoded directly
+  bool load(const char *path) {
+    const H5Api &a = h5();
+    if (!a.ok || !a.chunks) return false;
+    H5Field fld;
+    if (!fld.open(path)) return false;
+    for (int i = 0; i < 3; i++) dims[i] = fld.dims[i];
+    const hid_t_ ty = a.dget_type(fld.dset);
+    const bool f32 = a.tget_class(ty) == H5T_FLOAT_CLASS && a.tget_size(ty) == 4;
+    be = a.tget_order(ty) == 1;                   // H5T_ORDER_BE
+    a.tclose(ty);
+    if (!f32) return false;
+    const hid_t_ pl = a.dget_create_plist(fld.dset);
+    if (pl < 0) return false;
+    bool ok = a.pget_layout(pl) == 2 /* H5D_CHUNKED */ && a.pget_chunk(pl, 3, cd) == 3;
+    nfilt = ok ? a.pget_nfilters(pl) : -1;
+    ok = ok && nfilt >= 0 && nfilt <= 8;
+    for (int i = 0; ok && i < nfilt; i++) {
+      unsigned flags = 0, cdv[8], fcfg = 0;
+      size_t ncd = 8;
+      char nm[32];
+      filt[i] = a.pget_filter2(pl, (unsigned)i, &flags, &ncd, cdv, sizeof nm, nm, &fcfg);
+      ok = filt[i] == 1 /* H5Z_FILTER_DEFLATE */ || filt[i] == 2 /* H5Z_FILTER_SHUFFLE */;
+    }
+    a.pclose(pl);
+    if (!ok || !inflater().ok) return false;
+    hsize_t_ n = 0;
+    // (1.10.6 rejects H5S_ALL here: pass the dataset's own dataspace)
+    if (a.dget_num_chunks(fld.dset, fld.space, &n) < 0) return false;
+    ch.resize((size_t)n);
+    for (hsize_t_ i = 0; i < n; i++) {
+      Ch &c = ch[(size_t)i];
+      hsize_t_ sz = 0;
+      if (a.dget_chunk_info(fld.dset, fld.space, i, c.c, &c.mask, &c.addr, &sz) < 0) return false;
+      c.size = sz;
+    }
+    return true;
+  }
+  size_t chunk_bytes() const { return (size_t)(cd[0] * cd[1] * cd[2]) * 4; }
+  // Decodes a chunk.  The values end in *data: 4-byte elements, either
+  // plain or, when the last filter to undo is the shuffle, still as the
+  // shuffle's 4 byte planes -- the gather then reads each wanted element
+  // from the planes (value()), so only the cells' values are ever
+  // reassembled (a quarter of a 0.5 deg day).  raw and tmp are scratch.
+  struct View {
+    const unsigned char *p;
+    size_t ne;
+    bool planes, be;
+    float value(size_t e) const {
+      uint32_t u;
+      if (planes)
+        u = (uint32_t)p[e] | (uint32_t)p[ne + e] << 8 | (uint32_t)p[2 * ne + e] << 16 | (uint32_t)p[3 * ne + e] << 24;
+      else
+        memcpy(&u, p + 4 * e, 4);
+      if (be) u = __builtin_bswap32(u);
+      float f;
+      memcpy(&f, &u, 4);
+      return f;
+    }
+  };
+  bool decode(int fd, const Ch &c, std::vector<unsigned char> &raw, std::vector<unsigned char> &tmp, View &out,
+              void *&zst) const {
+    const size_t nb = chunk_bytes();
+    raw.resize((size_t)c.size);
+    if (pread(fd, raw.data(), (size_t)c.size, (off_t)c.addr) != (ssize_t)c.size) return false;
+    std::vector<unsigned char> *cur = &raw, *spare = &tmp;
+    bool planes = false;
+    for (int i = nfilt - 1; i >= 0; i--) {        // undo the pipeline in reverse
+      if (c.mask & (1u << i)) continue;           // filter skipped for this chunk
+      if (planes) {                               // a filter below the shuffle: reassemble first
+        spare->resize(nb);
+        const View v{cur->data(), nb / 4, true, false};
+        for (size_t e = 0; e < nb / 4; e++) {
+          const float f = v.value(e);
+          memcpy(spare->data() + 4 * e, &f, 4);
+        }
+        std::swap(cur, spare);
+        planes = false;
+      }
+      if (filt[i] == 1) {
+        spare->resize(nb);
+        if (!inflate_exact(zst, cur->data(), cur->size(), spare->data(), nb)) return false;
+        std::swap(cur, spare);
+      } else {
+        if (cur->size() != nb) return false;
+        planes = true;
+      }
+    }
+    if (cur->size() != nb) return false;
+    out = View{cur->data(), nb / 4, planes, be};
+    return true;
+  }
+};
+
+// Host threads of the ingest pool: $H9G_IO_THREADS, else the hardware's,
+// at most 16 (a GPU's share of the host on the MI355X boxes).
+int io_threads() {
+  if (const char *e = getenv("H9G_IO_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) return v;
+  }
+  const unsigned hc = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(16u, hc ? hc : 1u));
+}
+
+// Runs job(i, worker) for i in [0, n) on the pool; false if any job failed.
+template <class F>
+bool run_pool(size_t n, F job) {
+  const int nt = (int)std::min<size_t>((size_t)io_threads(), std::max<size_t>(n, 1));
+  std::atomic<size_t> next{0};
+  std::atomic<bool> ok{true};
+  auto work = [&](int w) {
+    for (size_t i; ok.load(std::memory_order_relaxed) && (i = next.fetch_add(1)) < n;)
+      if (!job(i, w)) ok = false;
+  };
+  std::vector<std::thread> th;
+  for (int w = 1; w < nt; w++) th.emplace_back(work, w);
+  work(0);
+  for (auto &t : th) t.join();
+  return ok;
 }
 
 // ------------------------------------------------------------------ writer
@@ -479,6 +698,15 @@ int write_cdf2(const char *path, const std::vector<std::pair<std::string, uint32
 // --------------------------------------------------------------- C-ABI
 extern "C" {
 
+#ifndef H9G_BUILD_ID
+#define H9G_BUILD_ID "unknown"
+#endif
+// Digest of the sources and flags this library was compiled from
+// (hybrid9_amd/build.py build_id); profiles record it, bench.py matches it.
+// Defined here, in the translation unit compiled last and in seconds, so
+// the device code's object is reused when only this digest changes.
+const char *h9g_build_id(void) { return H9G_BUILD_ID; }
+
 // WRITE_NET_CDF_3DR.f90: one year of annual means of the cells `gid`
 // (grid ids iy*nx+ix, latitude row iy from the north, INIT.f90:142-145) to
 // a CDF-2 file; every other grid cell is the NaN fill.
@@ -539,59 +767,204 @@ int h9g_write_axy_nc(const char *path, int nx, int ny, int nlayers, const float 
 // READ_PGF.f90 + READ_NET_CDF_3DR.f90 for the cells of a context: days
 // [t0, t0+nt) of the 7 files (READ_PGF order tas rlds rsds huss ps pr rhs),
 // variable 4 of each (dims time, lat, lon), gathered at the grid ids gid
-// into out (7, nt, ncell).  The 7 files are read on 7 host threads.
+// into out (7, nt, ncell).  Like the reference, which reads only its rank's
+// block (READ_NET_CDF_3DR.f90:95-97), only the rows spanning the cells are
+// decoded.  All work runs on one pool of host threads (io_threads):
+//   netCDF-4  one job per stored chunk holding any of the cells: pread, then
+//             inflate/unshuffle outside HDF5 (Chunked), then the gather;
+//             other layouts: one job per file through H5Dread, row band only
+//   classic   one job per (file, day): pread of the row band, byte swap of
+//             the gathered values.
 int h9g_nc_forcing_read(const char *const *paths, int nx, int ny, int ncell, const int64_t *gid, int t0,
                         int nt, float *out) {
-  if (!paths || nx <= 0 || ny <= 0 || ncell <= 0 || !gid || t0 < 0 || nt < 1 || !out) return H9G_EINVAL;
-  int rc[H9G_NFORCING];
-  std::vector<std::thread> th;
-  for (int k = 0; k < H9G_NFORCING; k++) {
-    rc[k] = 0;
-    th.emplace_back([&, k]() {
-      if (paths[k] && is_hdf5(paths[k])) {          // netCDF-4
-        H5Field fld;
-        if (!fld.open(paths[k]) || fld.dims[1] != (hsize_t_)ny || fld.dims[2] != (hsize_t_)nx ||
-            (hsize_t_)(t0 + nt) > fld.dims[0]) {
-          rc[k] = H9G_EINVAL;
-          return;
-        }
-        std::vector<float> slice((size_t)nx * ny);
-        for (int t = 0; t < nt; t++) {
-          if (!fld.read_day((hsize_t_)(t0 + t), slice.data())) { rc[k] = H9G_EINVAL; return; }
-          float *o = out + ((size_t)k * nt + t) * ncell;
-          for (int c = 0; c < ncell; c++) o[c] = slice[(size_t)gid[c]];
-        }
-        return;
-      }
-      NcReader r;
-      if (!paths[k] || !r.open(paths[k]) || r.vars.empty()) { rc[k] = H9G_EINVAL; return; }
-      // varid = 4 (READ_PGF.f90:30) when it is the (time, lat, lon) float
-      // field, as in the PGF files; otherwise the file's only such field
-      const int dt = r.dim_index("time");
-      auto is_field = [&](const NcVar &x) { return x.type == NC_FLOAT && x.dims.size() == 3 && x.dims[0] == dt; };
-      const NcVar *pv = &r.vars[r.vars.size() >= 4 ? 3 : 0];
-      if (!is_field(*pv))
-        for (auto &x : r.vars)
-          if (is_field(x)) { pv = &x; break; }
-      const NcVar &v = *pv;
-      if (v.type != NC_FLOAT || v.dims.size() != 3 || v.dims[0] != dt || r.dim_of(v, 1) != (uint64_t)ny ||
-          r.dim_of(v, 2) != (uint64_t)nx || (uint64_t)(t0 + nt) > r.dim_of(v, 0)) {
-        rc[k] = H9G_EINVAL;
-        return;
-      }
-      std::vector<float> slice((size_t)nx * ny);
-      for (int t = 0; t < nt; t++) {
-        if (!r.read_slice(v, (uint64_t)(t0 + t), slice.data())) { rc[k] = H9G_EINVAL; return; }
-        float *o = out + ((size_t)k * nt + t) * ncell;
-        for (int c = 0; c < ncell; c++) o[c] = slice[(size_t)gid[c]];
-      }
-    });
-  }
-  for (auto &t : th) t.join();
-  for (int k = 0; k < H9G_NFORCING; k++)
-    if (rc[k]) return rc[k];
-  return 0;
+  return h9g_nc_read_groups(paths, nx, ny, ncell, gid, t0, nt, out, 1, nullptr);
 }
+
+}  // extern "C"
+
+// The read of h9g_nc_forcing_read, reporting progress: the days are split
+// into ngroups consecutive groups, and done(d0, d1) is called (on a pool
+// thread, once per group, in any order) as soon as days [d0, d1) (relative
+// to t0) of all 7 variables are in `out` -- h9g_nc_forcing_prefetch queues
+// each group's copy to the device then, so the copies overlap the rest of
+// the read.  Jobs are issued in day order.
+int h9g_nc_read_groups(const char *const *paths, int nx, int ny, int ncell, const int64_t *gid, int t0, int nt,
+                       float *out, int ngroups, const std::function<void(int, int)> &done) {
+  if (!paths || nx <= 0 || ny <= 0 || ncell <= 0 || !gid || t0 < 0 || nt < 1 || !out) return H9G_EINVAL;
+  ngroups = std::max(1, std::min(ngroups, nt));
+  int64_t ymin = ny, ymax = -1;
+  for (int c = 0; c < ncell; c++) {
+    if (gid[c] < 0 || gid[c] >= (int64_t)nx * ny) return H9G_EINVAL;
+    ymin = std::min<int64_t>(ymin, gid[c] / nx);
+    ymax = std::max<int64_t>(ymax, gid[c] / nx);
+  }
+  const size_t plane = (size_t)nx * ny;
+  struct Src {
+    int kind = 0;            // 1 chunked netCDF-4, 2 other netCDF-4, 3 classic
+    int fd = -1;
+    Chunked ck;
+    NcReader nc;
+    const NcVar *v = nullptr;
+    ~Src() {
+      if (fd >= 0) close(fd);
+    }
+  };
+  std::vector<Src> src(H9G_NFORCING);
+  for (int k = 0; k < H9G_NFORCING; k++) {        // headers and chunk tables (HDF5 calls: serial)
+    Src &s = src[(size_t)k];
+    if (!paths[k]) return H9G_EINVAL;
+    if (is_hdf5(paths[k])) {
+      if (s.ck.load(paths[k])) {
+        s.kind = 1;
+        if ((s.fd = open(paths[k], O_RDONLY)) < 0) return H9G_EINVAL;
+      } else {
+        H5Field fld;
+        if (!fld.open(paths[k])) return H9G_EINVAL;
+        for (int i = 0; i < 3; i++) s.ck.dims[i] = fld.dims[i];
+        s.kind = 2;
+      }
+      if (s.ck.dims[1] != (hsize_t_)ny || s.ck.dims[2] != (hsize_t_)nx || (hsize_t_)(t0 + nt) > s.ck.dims[0])
+        return H9G_EINVAL;
+      continue;
+    }
+    NcReader &r = s.nc;
+    if (!r.open(paths[k]) || r.vars.empty()) return H9G_EINVAL;
+    // varid = 4 (READ_PGF.f90:30) when it is the (time, lat, lon) float
+    // field, as in the PGF files; otherwise the file's only such field
+    const int dt = r.dim_index("time");
+    auto is_field = [&](const NcVar &x) { return x.type == NC_FLOAT && x.dims.size() == 3 && x.dims[0] == dt; };
+    const NcVar *pv = &r.vars[r.vars.size() >= 4 ? 3 : 0];
+    if (!is_field(*pv))
+      for (auto &x : r.vars)
+        if (is_field(x)) { pv = &x; break; }
+    if (pv->type != NC_FLOAT || pv->dims.size() != 3 || pv->dims[0] != dt || r.dim_of(*pv, 1) != (uint64_t)ny ||
+        r.dim_of(*pv, 2) != (uint64_t)nx || (uint64_t)(t0 + nt) > r.dim_of(*pv, 0))
+      return H9G_EINVAL;
+    s.v = pv;
+    s.kind = 3;
+    if ((s.fd = open(paths[k], O_RDONLY)) < 0) return H9G_EINVAL;
+  }
+  // jobs: (file, chunk) for chunked files, (file, day) for classic, (file)
+  // otherwise; d0..d1: the days (relative to t0) a job fills
+  struct Job { int k; size_t i; int d0, d1; };
+  std::vector<Job> jobs;
+  // cells by chunk column (per chunked file's chunk shape; usually shared)
+  struct Cols {
+    hsize_t_ cy = 0, cx = 0;
+    size_t nbx = 0;
+    std::vector<std::vector<std::pair<int, uint32_t>>> cells;   // (cell, offset in the chunk's plane)
+  };
+  std::vector<Cols> cols(H9G_NFORCING);
+  for (int k = 0; k < H9G_NFORCING; k++) {
+    Src &s = src[(size_t)k];
+    if (s.kind == 1) {
+      Cols &cl = cols[(size_t)k];
+      cl.cy = s.ck.cd[1];
+      cl.cx = s.ck.cd[2];
+      cl.nbx = (size_t)((nx + cl.cx - 1) / cl.cx);
+      cl.cells.resize(cl.nbx * (size_t)((ny + cl.cy - 1) / cl.cy));
+      for (int c = 0; c < ncell; c++) {
+        const hsize_t_ y = (hsize_t_)(gid[c] / nx), x = (hsize_t_)(gid[c] % nx);
+        cl.cells[(size_t)(y / cl.cy) * cl.nbx + (size_t)(x / cl.cx)].push_back(
+            {c, (uint32_t)((y % cl.cy) * cl.cx + x % cl.cx)});
+      }
+      for (size_t i = 0; i < s.ck.ch.size(); i++) {
+        const auto &ch = s.ck.ch[i];
+        if (ch.c[0] + s.ck.cd[0] <= (hsize_t_)t0 || ch.c[0] >= (hsize_t_)(t0 + nt)) continue;
+        if (!cl.cells[(size_t)(ch.c[1] / cl.cy) * cl.nbx + (size_t)(ch.c[2] / cl.cx)].empty()) {
+          const int d0 = (int)std::max<hsize_t_>(ch.c[0], (hsize_t_)t0) - t0;
+          const int d1 = (int)std::min<hsize_t_>(ch.c[0] + s.ck.cd[0], (hsize_t_)(t0 + nt)) - t0;
+          jobs.push_back({k, i, d0, d1});
+        }
+      }
+    } else if (s.kind == 3) {
+      for (int t = 0; t < nt; t++) jobs.push_back({k, (size_t)t, t, t + 1});
+    } else {
+      jobs.push_back({k, 0, 0, nt});
+    }
+  }
+  std::stable_sort(jobs.begin(), jobs.end(), [](const Job &a, const Job &b) { return a.d0 < b.d0; });
+  // day groups [gd(g), gd(g+1)) and the jobs each still waits for
+  auto gd = [&](int g) { return (int)((long long)nt * g / ngroups); };
+  auto group_of = [&](int d) {                     // the group holding day d
+    int g = (int)((long long)d * ngroups / nt);
+    while (g + 1 < ngroups && gd(g + 1) <= d) g++;
+    while (g > 0 && gd(g) > d) g--;
+    return g;
+  };
+  std::vector<std::atomic<int>> pending((size_t)ngroups);
+  for (auto &p : pending) p = 0;
+  for (const Job &jb : jobs)
+    for (int g = group_of(jb.d0); g <= group_of(jb.d1 - 1); g++) pending[(size_t)g]++;
+  const int nw = io_threads();
+  struct Scratch {
+    std::vector<unsigned char> raw, tmp;
+    std::vector<float> vals;
+    void *z = nullptr;
+  };
+  std::vector<Scratch> scr((size_t)nw);
+  std::mutex h5lock;                                // kind 2 goes through HDF5
+  auto finish = [&](const Job &jb) {
+    for (int g = group_of(jb.d0); g <= group_of(jb.d1 - 1); g++)
+      if (--pending[(size_t)g] == 0 && done) done(gd(g), gd(g + 1));
+  };
+  auto one = [&](const Job &jb, Scratch &sc) -> bool {
+    Src &s = src[(size_t)jb.k];
+    if (s.kind == 1) {
+      const auto &ch = s.ck.ch[jb.i];
+      Chunked::View v;
+      if (!s.ck.decode(s.fd, ch, sc.raw, sc.tmp, v, sc.z)) return false;
+      const Cols &cl = cols[(size_t)jb.k];
+      const auto &cells = cl.cells[(size_t)(ch.c[1] / cl.cy) * cl.nbx + (size_t)(ch.c[2] / cl.cx)];
+      const size_t cplane = (size_t)(cl.cy * cl.cx);
+      const hsize_t_ ta = std::max<hsize_t_>(ch.c[0], (hsize_t_)t0);
+      const hsize_t_ tb = std::min<hsize_t_>(ch.c[0] + s.ck.cd[0], (hsize_t_)(t0 + nt));
+      for (hsize_t_ t = ta; t < tb; t++) {
+        const size_t e0 = (size_t)(t - ch.c[0]) * cplane;
+        float *o = out + ((size_t)jb.k * nt + (size_t)(t - (hsize_t_)t0)) * ncell;
+        for (const auto &p : cells) o[p.first] = v.value(e0 + p.second);
+      }
+      return true;
+    }
+    if (s.kind == 3) {                              // classic: rows [ymin, ymax] of day t0 + i
+      const NcReader &r = s.nc;
+      const NcVar &v = *s.v;
+      const uint64_t t = (uint64_t)t0 + jb.i;
+      const uint64_t off = (v.record ? v.begin + t * r.recsize : v.begin + t * plane * 4) + (uint64_t)ymin * nx * 4;
+      const size_t nb = (size_t)(ymax - ymin + 1) * nx * 4;
+      sc.raw.resize(nb);
+      if (pread(s.fd, sc.raw.data(), nb, (off_t)off) != (ssize_t)nb) return false;
+      const uint32_t *u = (const uint32_t *)sc.raw.data();
+      uint32_t *o = (uint32_t *)(out + ((size_t)jb.k * nt + jb.i) * ncell);
+      const size_t base = (size_t)ymin * nx;
+      for (int c = 0; c < ncell; c++) o[c] = __builtin_bswap32(u[(size_t)gid[c] - base]);
+      return true;
+    }
+    // netCDF-4 of another layout: H5Dread of the row band, day by day
+    std::lock_guard<std::mutex> g(h5lock);
+    H5Field fld;
+    if (!fld.open(paths[jb.k])) return false;
+    const hsize_t_ nyb = (hsize_t_)(ymax - ymin + 1);
+    sc.vals.resize((size_t)nyb * nx);
+    for (int t = 0; t < nt; t++) {
+      if (!fld.read_rows((hsize_t_)(t0 + t), (hsize_t_)ymin, nyb, sc.vals.data())) return false;
+      float *o = out + ((size_t)jb.k * nt + t) * ncell;
+      const size_t base = (size_t)ymin * nx;
+      for (int c = 0; c < ncell; c++) o[c] = sc.vals[(size_t)gid[c] - base];
+    }
+    return true;
+  };
+  const bool ok = run_pool(jobs.size(), [&](size_t j, int w) -> bool {
+    if (!one(jobs[j], scr[(size_t)w % scr.size()])) return false;
+    finish(jobs[j]);
+    return true;
+  });
+  for (auto &sc : scr)
+    if (sc.z && inflater().release) inflater().release(sc.z);
+  return ok ? 0 : H9G_EINVAL;
+}
+
+extern "C" {
 
 // NTIMES of a PGF file (READ_NET_CDF_0D.f90: the 'time' dimension).
 int h9g_nc_ntimes(const char *path) {

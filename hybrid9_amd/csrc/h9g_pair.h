@@ -1592,9 +1592,19 @@ H9K_RARE int substep_exact_pair(const G *g, CS cs, const uint64_t *e2, const dou
 
 // Substep ns of the day on the fast path.  A pair re-runs (exactly, from the
 // day snapshot) if either of its lanes needs a third water-table layer visit.
+// `snapped`: the day snapshot was taken today, at or before this substep.
+// Only a substep that starts with the water table in the column (jwt < L)
+// can ask for the re-run -- the rising/deepening loops run only for jwt < L
+// and the drainage loop only for jwt2 < L, where HYDROLOGY.f90 recomputes
+// jwt2 only in the jwt < L branch (:995-1005), so a substep starting below
+// the column keeps jwt2 = L -- and cell_year_pair snapshots before the
+// first such substep of the day.  A request without a snapshot would replay
+// another day's (or, after the yearly re-sort, another cell's) block: it is
+// reported as H9G_ERR_NOSNAP instead (never raised by a correct
+// build, tests/test_kernel_host.py forces it).
 template <int L, class G, class SP, class CS, class PR>
 H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_sum, float &errval,
-                        const h9m::Tabs &T, PR &pr, int ns) {
+                        const h9m::Tabs &T, PR &pr, int ns, bool snapped) {
   pr.mark(0);
   H9G_BR(BR_SUBSTEP);
 #if defined(H9G_ISA_MARK) && defined(__HIP_DEVICE_COMPILE__)
@@ -1603,6 +1613,8 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
   MathFast mf{T, false};
 #if defined(H9G_FORCE_RERUN)
   const bool in_column = s.zwt <= g.zim(L);   // the substeps that may re-run (cell_year_pair)
+#elif defined(H9G_FORCE_RERUN_ANY)
+  const bool in_column = true;                // test builds: also below the column (-> H9G_ERR_NOSNAP)
 #endif
   int code = hydrology_pair<L, G, MathFast, SP, CS, PR>(g, cs, sp, s, rnf_sum, errval, mf, pr);
 #if defined(H9G_FORCE_RERUN)
@@ -1610,9 +1622,15 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
   // could (the exact replay from the day snapshot must reproduce the fast
   // path's state)
   if (in_column && ns % H9G_FORCE_RERUN == H9G_FORCE_RERUN - 1) mf.special = true;
+#elif defined(H9G_FORCE_RERUN_ANY)
+  if (in_column && ns % H9G_FORCE_RERUN_ANY == H9G_FORCE_RERUN_ANY - 1) mf.special = true;
 #endif
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
     H9G_BR(BR_RERUN);
+    if (!snapped) {                          // no snapshot of today to replay from
+      errval = (float)ns;
+      return H9G_ERR_NOSNAP_K;
+    }
 #if defined(H9G_COUNT_EXACT) && defined(__HIP_DEVICE_COMPILE__)
     atomicAdd(&h9g_exact_count, 1ull);      // measurement builds only
     atomicAdd(&h9g_exact_wave[(blockIdx.x * 4 + (threadIdx.x >> 6)) & 0xffff], 1u);
@@ -1709,7 +1727,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
         save_day<L>(sp, cs, s, rnf_sum, ns);
         snapped = true;
       }
-      code = substep_pair<L, G, SP, CS>(g, cs, sp, s, rnf_sum, errval, T, pr, ns);
+      code = substep_pair<L, G, SP, CS>(g, cs, sp, s, rnf_sum, errval, T, pr, ns, snapped);
       if (code) { eday = day; estep = ns; break; }
     }
     cs.launder();

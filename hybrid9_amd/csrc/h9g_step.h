@@ -39,6 +39,8 @@
 namespace h9k {
 
 constexpr float zero = 0.0f, one = 1.0f;
+// include/h9g.h H9G_ERR_NOSNAP (the host build does not include h9g.h)
+constexpr int H9G_ERR_NOSNAP_K = 5;
 constexpr float rhow = 1000.0f;
 constexpr float gasc = 8.314510f;
 constexpr float rgas = 0x1.1f0c7cp+8f;     // 1000*gasc/mair (SHARED.f90:335)

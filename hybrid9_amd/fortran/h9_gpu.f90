@@ -16,6 +16,7 @@ INTEGER, PARAMETER :: H9G_LMAX = 10
 INTEGER, PARAMETER :: H9G_NDIAG = 12
 INTEGER, PARAMETER :: H9G_ERR_TRIDIAG1 = 1, H9G_ERR_TRIDIAG2 = 2
 INTEGER, PARAMETER :: H9G_ERR_RSUB_POS = 3, H9G_ERR_IMBALANCE = 4
+INTEGER, PARAMETER :: H9G_ERR_NOSNAP = 5   ! internal invariant, not a reference STOP
 
 TYPE, BIND(C) :: h9g_config
   INTEGER(C_INT32_T) :: ncell, nlayers, nisurf, grow_on, max_days, nslots
@@ -308,6 +309,8 @@ CONTAINS
     CASE (H9G_ERR_RSUB_POS)
       WRITE (*,*) 'rsub_top_tot is positive in drainage'
       WRITE (*,*) 'HYBRID9 is stopping'
+    CASE (H9G_ERR_NOSNAP)
+      WRITE (*,*) 'h9g internal: exact re-run with no day snapshot'
     CASE DEFAULT
       WRITE (*,*) 'Problem in HYDROLOGY'
       WRITE (*,*) 'Water imbalance > 0.1 mm ', e%value

@@ -48,6 +48,10 @@ extern "C" {
 #define H9G_ERR_TRIDIAG2 2   /* :818-825  zero pivot             */
 #define H9G_ERR_RSUB_POS 3   /* :1068-1072 rsub_top_tot > 0      */
 #define H9G_ERR_IMBALANCE 4  /* :1244-1274 |w1 - w0| > 0.1 mm    */
+/* not a reference STOP: the pair kernel's exact re-run was requested in a
+ * substep with no day snapshot to replay from (an internal invariant,
+ * DESIGN.md §3 "Day snapshot"; never raised by a correct build) */
+#define H9G_ERR_NOSNAP 5
 /* API / runtime failures */
 #define H9G_EINVAL (-1)
 #define H9G_EHIP (-2)

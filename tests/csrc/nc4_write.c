@@ -5,11 +5,17 @@
  * path of h9g_io.cpp is tested on the on-disk form of a PGF v2.1 file
  * (READ_NET_CDF_3DR.f90:95-97 reads it with nf90_get_var).
  *   nc4_write <path> <name> <nt> <ny> <nx> <raw float32 file (nt*ny*nx)>
+ *             [ct cy cx [filters]]
+ * Optional: the chunk shape (default 1, ny, nx: one chunk per day) and the
+ * filters, letters of "s" shuffle, "d" deflate 4, "f" fletcher32, "b" a
+ * big-endian field (default "sd"), so every layout the reader's direct
+ * chunk path and its H5Dread fallback take can be written.
  * Built by tests/test_netcdf.py: gcc ... -lhdf5_hl -lhdf5 (/opt/conda). */
 #include <hdf5.h>
 #include <hdf5_hl.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 static hid_t coord(hid_t f, const char *name, hsize_t n, const float *v) {
   hid_t sp = H5Screate_simple(1, &n, NULL);
@@ -21,7 +27,7 @@ static hid_t coord(hid_t f, const char *name, hsize_t n, const float *v) {
 }
 
 int main(int argc, char **argv) {
-  if (argc != 7) return 2;
+  if (argc != 7 && argc != 10 && argc != 11) return 2;
   const hsize_t nt = atoi(argv[3]), ny = atoi(argv[4]), nx = atoi(argv[5]);
   float *data = malloc(sizeof(float) * nt * ny * nx);
   FILE *in = fopen(argv[6], "rb");
@@ -38,12 +44,22 @@ int main(int argc, char **argv) {
   for (hsize_t i = 0; i < nx; i++) xv[i] = -180.0f + (i + 0.5f) * 360.0f / nx;
   hid_t dt = coord(f, "time", nt, tv), dy = coord(f, "lat", ny, yv), dx = coord(f, "lon", nx, xv);
   hsize_t dims[3] = {nt, ny, nx}, chunk[3] = {1, ny, nx};
+  const char *filt = argc == 11 ? argv[10] : "sd";
+  if (argc >= 10) {
+    chunk[0] = atoi(argv[7]);
+    chunk[1] = atoi(argv[8]);
+    chunk[2] = atoi(argv[9]);
+  }
   hid_t sp = H5Screate_simple(3, dims, NULL);
   hid_t dcpl = H5Pcreate(H5P_DATASET_CREATE);
   H5Pset_chunk(dcpl, 3, chunk);
-  H5Pset_shuffle(dcpl);
-  H5Pset_deflate(dcpl, 4);
-  hid_t dv = H5Dcreate2(f, argv[2], H5T_IEEE_F32LE, sp, H5P_DEFAULT, dcpl, H5P_DEFAULT);
+  for (const char *c = filt; *c; c++) {
+    if (*c == 's') H5Pset_shuffle(dcpl);
+    if (*c == 'd') H5Pset_deflate(dcpl, 4);
+    if (*c == 'f') H5Pset_fletcher32(dcpl);
+  }
+  const hid_t ftype = strchr(filt, 'b') ? H5T_IEEE_F32BE : H5T_IEEE_F32LE;
+  hid_t dv = H5Dcreate2(f, argv[2], ftype, sp, H5P_DEFAULT, dcpl, H5P_DEFAULT);
   H5Dwrite(dv, H5T_NATIVE_FLOAT, H5S_ALL, H5S_ALL, H5P_DEFAULT, data);
   H5DSattach_scale(dv, dt, 0);
   H5DSattach_scale(dv, dy, 1);

@@ -94,13 +94,19 @@ def nc4_writer_bin() -> Path | None:
                              f"-L{CONDA}/lib", f"-Wl,-rpath,{CONDA}/lib", "-lhdf5_hl", "-lhdf5"])
 
 
-def write_nc4(path: Path, var: str, data: np.ndarray) -> Path:
+def write_nc4(path: Path, var: str, data: np.ndarray, chunk=None, filters: str | None = None) -> Path:
     """A netCDF-4 (HDF5) file with <var>(time, lat, lon) and its coordinate
-    dimension scales (nc4_write.c)."""
+    dimension scales (nc4_write.c); chunk (ct, cy, cx) and filters
+    ("s" shuffle, "d" deflate, "f" fletcher32, "b" big-endian) default to one
+    chunk per day, shuffle + deflate."""
     exe = nc4_writer_bin()
     raw = path.with_suffix(".raw")
     np.ascontiguousarray(data, np.float32).tofile(raw)
     nt, ny, nx = data.shape
-    subprocess.run([str(exe), str(path), var, str(nt), str(ny), str(nx), str(raw)], check=True)
+    extra = []
+    if chunk is not None or filters is not None:
+        ct, cy, cx = chunk if chunk is not None else (1, ny, nx)
+        extra = [str(ct), str(cy), str(cx)] + ([filters] if filters is not None else [])
+    subprocess.run([str(exe), str(path), var, str(nt), str(ny), str(nx), str(raw), *extra], check=True)
     raw.unlink()
     return path

@@ -141,3 +141,22 @@ def test_exact_rerun_replays_from_day_snapshot(name):
     assert same_bits(out["annual"], exp["annual"]) and same_bits(out["state"], exp["state"])
     runs, multi, replayed = st
     assert runs > 100 and multi > 0 and replayed > 4 * runs, st
+
+
+def test_rerun_without_day_snapshot_is_reported():
+    """an exact re-run requested in a substep that has no day
+    snapshot (the water table started below the column, jwt = L) must not
+    replay a stale snapshot block.  Such a request cannot arise (only a
+    substep starting with jwt < L visits layers, h9g_pair.h substep_pair), so
+    a test build forces one at every 5th substep regardless of where the
+    water table is: every c1_10x10 cell starts below the column (INIT.f90:
+    zwt = (zi(L) + 5000)/1000 m), so each must stop with H9G_ERR_NOSNAP on day
+    0, substep 4, instead of running on."""
+    so = C.CDLL(str(_build_lib(["-DH9G_FORCE_RERUN_ANY=5"])))
+    so.h9k_host_run.argtypes = lib().h9k_host_run.argtypes
+    meta, inp, exp = load_golden("c1_10x10")
+    out = host_run(const_geo=1, so=so, **inp)
+    assert out["rc"] == 5                                  # include/h9g.h H9G_ERR_NOSNAP
+    err = out["err"]
+    assert (err[:, 0] == 5).all() and (err[:, 1] == 0).all()
+    assert (err[:, 2] == 0).all() and (err[:, 3] == 4).all()
