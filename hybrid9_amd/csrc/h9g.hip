@@ -120,11 +120,9 @@ __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
 template <int L>
 constexpr int pair_waves() { return pair_resident<L>(); }
 
-template <int L, class G>
-__global__ void __launch_bounds__(64 * H9G_PWAVES)
-    __attribute__((amdgpu_waves_per_eu(pair_waves<L>(), pair_waves<L>())))
-h9g_pair_kernel(const KArgs a, const G g) {
-  typedef PairStore<L, H9G_PLANES> PS;
+template <int L, class G, int R>
+__device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
+  typedef PairStore<L, H9G_PLANES, R> PS;
   __shared__ uint64_t s_e2[32];
   __shared__ double s_l2[32];
   __shared__ float s_cell[H9G_PWAVES][PS::ROWS * H9G_PLANES];   // [wave][row][lane]
@@ -228,6 +226,25 @@ h9g_pair_kernel(const KArgs a, const G g) {
     for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + iow] = __builtin_nanf("");
   }
 }
+
+template <int L, class G>
+__global__ void __launch_bounds__(64 * H9G_PWAVES)
+    __attribute__((amdgpu_waves_per_eu(pair_waves<L>(), pair_waves<L>())))
+h9g_pair_kernel(const KArgs a, const G g) {
+  pair_body<L, G, pair_waves<L>()>(a, g);
+}
+
+// The pair kernel built for 2 waves per SIMD (round 4):
+// 256 VGPRs, so the L = 10 substep does not spill (the 3-wave build spills
+// 108 VGPRs and 118 SGPRs into a 296-B-per-lane scratch that reaches HBM),
+// and 80 KB of LDS per workgroup, so every reciprocal field fits.  It trades
+// a third of the resident waves for that; l10_kind picks it by shard size.
+template <int L, class G>
+__global__ void __launch_bounds__(64 * H9G_PWAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
+h9g_pair2_kernel(const KArgs a, const G g) {
+  pair_body<L, G, 2>(a, g);
+}
+
 
 // Solo kernel: one lane per soil column running the generic code of
 // h9g_pair.h with one lane doing every layer (SplitAll: two layers per
@@ -747,7 +764,6 @@ __global__ void h9g_soil_seq_kernel(int nx, int ncell, const int64_t *__restrict
   SoilOut::store(par, L, layer, (size_t)ncell, c, v, sum, j);
 }
 
-// MathFast's division path with a device-computed reciprocal (recip64).
 // Probe of the hardware ids pace_key decodes (h9g_pair.h): the
 // pair kernel's launch shape and LDS footprint (dynamic LDS of the same size,
 // so the same workgroups per CU), each wave's lane 0 arriving at a bounded
@@ -771,6 +787,7 @@ __global__ void __launch_bounds__(64 * H9G_PWAVES) h9g_pace_probe_kernel(unsigne
   out[3 * w + 2] = seen >= total ? 1u : 0u;
 }
 
+// MathFast's division path with a device-computed reciprocal (recip64).
 __global__ void h9g_div_kernel(int n, const float *x, const float *d, float *out, int *flag) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -849,7 +866,8 @@ struct h9g_ctx {
   int ncu = 256;
   int sort = 1;                   // H9G_SORT=0: identity order
   size_t sv_bytes = 0;
-  int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel, 3: both (H9G_KERNEL=pair|solo|mixed; default by L)
+  int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel, 3: both, 4: h9g_pair2_kernel (L = 10)
+                       // (H9G_KERNEL=pair|solo|mixed|pair2; default by L and the shard size, l10_kind)
   size_t n_solo = 0;   // kind 3: cells [0, n_solo) run on the solo kernel, the rest on the pair kernel
 };
 
@@ -920,10 +938,32 @@ static GeoKind geo_kind(const h9g_config &c) {
   } while (0)
 #endif
 
+// Launch a kernel that exists at L = 10 only (h9g_pair2_kernel).
+#if defined(H9G_ONLY_C2)
+#define H9G_DISPATCH_L10(ctx, KERNEL, GRID, BLOCK, STREAM, ...) \
+  do {                                                          \
+    fprintf(stderr, "h9g: H9G_ONLY_C2 build runs config 2 only\n"); \
+    return H9G_EINVAL;                                          \
+  } while (0)
+#else
+#define H9G_DISPATCH_L10(ctx, KERNEL, GRID, BLOCK, STREAM, ...)                         \
+  do {                                                                              \
+    const GeoKind gk_ = geo_kind((ctx)->cfg);                                       \
+    if (gk_ == GEO_C48)                                                             \
+      KERNEL<10, GeoC<10, 48>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__, GeoC<10, 48>()); \
+    else if (gk_ == GEO_C24)                                                        \
+      KERNEL<10, GeoC<10, 24>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__, GeoC<10, 24>()); \
+    else                                                                            \
+      KERNEL<10, GeoR<10>><<<GRID, BLOCK, 0, STREAM>>>(__VA_ARGS__,                 \
+                                                       make_geo_r<10>((ctx)->cfg.zi, (ctx)->cfg.nisurf)); \
+  } while (0)
+#endif
+
 #if defined(H9G_ISA_ONLY)
 // tools/isa_pair.sh: device code of the config-2 pair kernel alone (ISA study)
 #if defined(H9G_ISA_L10)
 template __global__ void h9g_pair_kernel<10, GeoC<10, 24>>(const KArgs, const GeoC<10, 24>);
+template __global__ void h9g_pair2_kernel<10, GeoC<10, 24>>(const KArgs, const GeoC<10, 24>);
 #else
 template __global__ void h9g_pair_kernel<8, GeoC<8, 48>>(const KArgs, const GeoC<8, 48>);
 #endif
@@ -994,10 +1034,16 @@ void h9g_destroy(h9g_ctx *ctx) {
 // round 2's rounds model picked solo at 33,750 cells (24% slower there).
 // Solo and mixed stay selectable (H9G_KERNEL) and are tested.  *n_solo:
 // the whole solo rounds (kind 3 only).
+// Round 4 adds the pair kernel built for 2 waves per SIMD (kind 4, 256
+// VGPRs: no spills, every reciprocal): where the shard's pair workgroups fit
+// one round of 2 per CU it is the faster one (33,750 cells: 98.1 vs 100.9 ms
+// per year), and wherever they do not it needs an extra round (270,000 cells:
+// 601.5 vs 505.8 ms), profiles/r04*_l10_shards.txt.
 static int l10_kind(size_t n, int ncu, size_t *n_solo) {
   const size_t solo_round = (size_t)4 * ncu * H9G_YBLOCK;
   *n_solo = (n / solo_round) * solo_round;
-  return 1;
+  const size_t blocks = (n + (size_t)H9G_PCPW * H9G_PWAVES - 1) / ((size_t)H9G_PCPW * H9G_PWAVES);
+  return blocks <= (size_t)2 * ncu ? 4 : 1;
 }
 
 // Device bytes a context of this configuration allocates: h9g_create's
@@ -1116,7 +1162,7 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     h9g_destroy(ctx);
     return nullptr;
   }
-  static const char *names[4][2][3] = {
+  static const char *names[5][2][3] = {
       {{"", "", ""}, {"", "", ""}},
       {{"h9g_pair_kernel<8,GeoR>", "h9g_pair_kernel<8,GeoC<8,24>>", "h9g_pair_kernel<8,GeoC<8,48>>"},
        {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}},
@@ -1126,7 +1172,9 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
         "h9g_solo_kernel<8,GeoC<8,48>>+h9g_pair_kernel<8,GeoC<8,48>>"},
        {"h9g_solo_kernel<10,GeoR>+h9g_pair_kernel<10,GeoR>",
         "h9g_solo_kernel<10,GeoC<10,24>>+h9g_pair_kernel<10,GeoC<10,24>>",
-        "h9g_solo_kernel<10,GeoC<10,48>>+h9g_pair_kernel<10,GeoC<10,48>>"}}};
+        "h9g_solo_kernel<10,GeoC<10,48>>+h9g_pair_kernel<10,GeoC<10,48>>"}},
+      {{"", "", ""},
+       {"h9g_pair2_kernel<10,GeoR>", "h9g_pair2_kernel<10,GeoC<10,24>>", "h9g_pair2_kernel<10,GeoC<10,48>>"}}};
   // default: the pair kernel at L = 8; at L = 10 the kernel that needs less
   // time for this many columns (l10_kind)
   if (const char *se = getenv("H9G_SORT")) ctx->sort = atoi(se) != 0;
@@ -1136,10 +1184,25 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1)
     ncu = 256;
   ctx->ncu = ncu;
+  // The XCD-aware orders (xcd_vwg, h9g_sort_kernel, h9g_perm_forcing_kernel)
+  // assume H9G_NXCD = 8 XCDs dealt round-robin, i.e. the MI355X in SPX mode
+  // (256 CUs).  Results never depend on it (every mapping is a permutation);
+  // only the per-XCD L2 locality does.  Say so once if the device differs
+  // (a CPX partition has one XCD of 32 CUs).
+  if (ncu != 32 * H9G_NXCD) {
+    static bool said = false;
+    if (!said) {
+      fprintf(stderr, "h9g: device %d has %d CUs, not %d: XCD-aware cell orders assume %d XCDs (SPX); results are "
+                      "unaffected, L2 locality may not hold\n", device, ncu, 32 * H9G_NXCD, H9G_NXCD);
+      said = true;
+    }
+  }
   if (kenv && strcmp(kenv, "solo") == 0)
     ctx->kind = 2;
   else if (kenv && strcmp(kenv, "pair") == 0)
     ctx->kind = 1;
+  else if (kenv && strcmp(kenv, "pair2") == 0 && L == 10)
+    ctx->kind = 4;
   else if (kenv && strcmp(kenv, "mixed") == 0) {
     // forced split (tests): H9G_SPLIT cells on the solo kernel, else the model's
     ctx->kind = 3;
@@ -1313,7 +1376,8 @@ static int pace_mode(const h9g_ctx *ctx, size_t m) {
   if (ctx->prio_mode >= 0) return ctx->prio_mode;
   const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
   const size_t blocks = (m + per_block - 1) / per_block;
-  return blocks <= (size_t)ctx->ncu * (ctx->L <= 8 ? pair_resident<8>() : pair_resident<10>()) ? 2 : 1;
+  const int resident = ctx->kind == 4 ? 2 : (ctx->L <= 8 ? pair_resident<8>() : pair_resident<10>());
+  return blocks <= (size_t)ctx->ncu * resident ? 2 : 1;
 }
 
 int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
@@ -1463,6 +1527,10 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
       H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n - ns + per_block - 1) / per_block), 64 * H9G_PWAVES,
                    ctx->sc, a);
     }
+  } else if (ctx->kind == 4) {
+    const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
+    H9G_DISPATCH_L10(ctx, h9g_pair2_kernel, (unsigned)((ctx->n + per_block - 1) / per_block), 64 * H9G_PWAVES,
+                     ctx->sc, a);
   } else {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n + per_block - 1) / per_block), 64 * H9G_PWAVES,

@@ -78,6 +78,9 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
 #ifndef H9G_FE_HK
 #define H9G_FE_HK 1   // ... of the conductivity / matric-potential slots
 #endif
+#ifndef H9G_FE2
+#define H9G_FE2 1     // both, in the 2-wave build (PairStore R = 2)
+#endif
 
 template <int K>
 struct FV {
@@ -129,6 +132,7 @@ H9K_HD float hi_d(double v) {
 template <int L>
 struct FlatStore {                     // host: one flat array per cell
   static constexpr bool kRecip = true, kRts = true, kDayRecip = true, kRtsHK = true;
+  static constexpr int FE_EQ = 1, FE_HK = 1;
   static constexpr int N = PF_N * L + PS_N;
   float *b;
   const float *zt;                     // zi(0..L+1), then zi(0..L+1)/1000
@@ -175,9 +179,10 @@ struct FlatStore {                     // host: one flat array per cell
 // cell), in a per-workgroup block shaped like the LDS block: the byte
 // offset of a value is its LDS address, so every snapshot store is
 // `global_store v_lds_address, s_block + imm` with no address arithmetic.
-// That leaves LDS room, within 3 workgroups per CU (76 rows per wave), for
+// That leaves LDS room, within 3 workgroups per CU (75 rows per wave), for
 // the reciprocal fields: 1/(-psi) at any L, 1/theta_s and the day
-// reciprocals at L = 8 (76 rows; L = 10: 73 rows).
+// reciprocals at L = 8 (75 rows; L = 10: 72 rows; the 2-wave build: all of
+// them at L = 10 too, 89 rows).
 // Issue priority of the waves sharing a SIMD (one from each of the CU's
 // resident workgroups).  The SIMD arbitrates VALU issue by priority, then by
 // wave age, so with equal priorities the oldest wave runs at its lone-wave
@@ -251,14 +256,19 @@ __device__ __forceinline__ void pace_key(int &row, int &slot) {
 template <int L>
 constexpr int pair_resident() { return 3; }   // waves per SIMD (h9g.hip pair_waves)
 
-template <int L, int S>
+// R = waves per SIMD the kernel is built for (its workgroups per CU): 3 (the
+// default, 168 VGPRs, <= 53 KB LDS per workgroup) or 2 (round 4, L = 10:
+// 256 VGPRs and 80 KB, so no spills and every reciprocal field; h9g.hip
+// h9g_pair2_kernel).
+template <int L, int S, int R = pair_resident<L>()>
 struct PairStore {
   static constexpr int NT = L / 2;
   // LDS fields by layer count (3 workgroups per CU: at most 75 rows).  L = 8:
   // every reciprocal (75 rows).  L = 10 (5 rows per per-layer field): 1/(-psi)
   // (~15 divisions per substep) instead of the day constants' reciprocals (~5;
-  // round 3: 533.6 -> 530.3 ms for config 5), no 1/theta_s (72 rows).
-  static constexpr bool kRecip = true, kRts = L <= 8, kDayRecip = L <= 8;
+  // round 3: 533.6 -> 530.3 ms for config 5), no 1/theta_s (72 rows).  At
+  // R = 2 every reciprocal fits at L = 10 too (89 rows).
+  static constexpr bool kRecip = true, kRts = L <= 8 || R <= 2, kDayRecip = L <= 8 || R <= 2;
   // s_node of the conductivity phase from the stored 1/theta_s too (round 3:
   // no longer spills in the call-free kernel)
   static constexpr bool kRtsHK = kRts;
@@ -269,7 +279,11 @@ struct PairStore {
   lds_float *self, *even;
   const lds_float *zt;                 // zi(0..L+1), then zi(0..L+1)/1000 (per block)
   float *svw;                          // this workgroup's day-snapshot block (global)
-  static constexpr int RESIDENT = pair_resident<L>();       // workgroups per CU = waves per SIMD (h9g.hip pair_waves)
+  static constexpr int RESIDENT = R;                        // workgroups per CU = waves per SIMD
+  // fence intervals of the per-layer phases' slots (Split2::par_d): one slot
+  // per scheduling region at 3 waves per SIMD (wider regions spill, DESIGN.md
+  // §3); the 2-wave build has the registers for H9G_FE2 slots per region
+  static constexpr int FE_EQ = R <= 2 ? H9G_FE2 : H9G_FE_EQ, FE_HK = R <= 2 ? H9G_FE2 : H9G_FE_HK;
   Pacer pace;
   __device__ __forceinline__ void day_start(int day) const { pace.day_start(day, RESIDENT); }
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
@@ -347,6 +361,7 @@ struct PairStore {
 template <int L>
 struct SoloStore {
   static constexpr bool kRecip = false, kRts = false, kDayRecip = false, kRtsHK = false;
+  static constexpr int FE_EQ = 1, FE_HK = 1;
   static constexpr int NPF = PF_RPSI0 + 2;           // TS..ROOTR, SVH2O, SVSMP
   static constexpr int NPS = PS_LAI + 5;             // FMAX..DAY, SV*
   static constexpr int ROWS = NPF * L + NPS;
@@ -438,6 +453,7 @@ struct StampProf {                     // wave-uniform shader-clock deltas per p
 // ---------------------------------------------------------------- policies
 // One lane computes every layer.
 struct SplitAll {
+  H9K_HD SplitAll fresh() const { return *this; }
   template <class CS>
   H9K_HD float own(const CS &cs, int p, int t, int h) const { return cs.lay(p, 2 * t + 1 + h); }
   // out[2t+1+h] = f(t, h).f for every layer; K outputs per layer
@@ -489,6 +505,11 @@ struct SplitAll {
 // Two lanes per column (device fast path); h = lane & 1.
 struct Split2 {
   int h;
+  H9K_HD Split2 fresh() const {   // h, opaque to the optimiser (hydrology_pair)
+    Split2 r{h};
+    opaque(r.h);
+    return r;
+  }
   // v of the even lane -> e, of the odd lane -> o, in both lanes: two DPP
   // broadcasts (round 3; round 2 swapped and selected per lane: one DPP
   // move and two selects, 214.5 -> 213.9 ms)
@@ -676,9 +697,17 @@ H9K_HD void cell_inv_pair(const G &g, const CS &cs) {
 // Split2 the per-layer phases are split over the pair (file comment).
 // The end-of-step theta(1..L) of :1233 is left to the caller (end_theta).
 template <int L, class G, class M, class SP, class CS, class PR = NoProf>
-H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_sum, float &errval,
+H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf_sum, float &errval,
                           M &m, PR &pr) {
   constexpr int NT = L / 2;
+  // At L = 10 the lane parity is made opaque here, so that values that
+  // depend only on it -- a lane's geometry-table offsets of its own layers,
+  // one per slot -- are recomputed inside the substep (an add each) instead
+  // of hoisted out of the year loop, spilled to scratch and reloaded behind
+  // a vmcnt(0) in every slot (round 4: scratch ops in the L = 10 substep
+  // loop 11.2 -> 6.7 per wave-substep, tools/isa_mix.py; at L = 8 nothing
+  // is hoisted that way and the change would only add VALU).
+  const SP sp = L >= 10 ? sp0.fresh() : sp0;
   const float dt = g.dt();
   constexpr double r1000 = 1.0 / 1000.0;
   float zim[L + 1];
@@ -1002,9 +1031,9 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_
     };
     // (round 3: the two phases' slots interleaved in one region, twice the
     // independent powers per region, spilled 225 VGPRs: 214.5 vs 208.9 ms)
-    sp.template par_d<NT, 1, H9G_FE_EQ>(eq_fast, eq_exact, outq);
+    sp.template par_d<NT, 1, CS::FE_EQ>(eq_fast, eq_exact, outq);
     pr.mark(2);
-    sp.template par_d<NT, 4, H9G_FE_HK>(hk_fast, hk_exact, outk);
+    sp.template par_d<NT, 4, CS::FE_HK>(hk_fast, hk_exact, outk);
   }
   // First round of single powers, one per lane, chosen by where the lane's
   // water table is (jwt = L: below the column), with the lane's operands:

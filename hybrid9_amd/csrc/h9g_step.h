@@ -214,7 +214,12 @@ struct MathExact {
 // make no calls.  Round 2 kept them out of line; the kernels' calls were
 // miscompiled: a lane-mask SGPR stayed live across calls to the redo
 // function, which overwrites it (tools/isa_calls.py).
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(H9G_RARE_CALLS)
+// reproducer of the round-2 miscompile: the rare paths out of
+// line again; tools/isa_calls.py --live then finds SGPRs live across calls
+// that the callee writes.  Never a product build.
+#define H9K_RARE __device__ __attribute__((noinline, cold))
+#elif defined(__HIP_DEVICE_COMPILE__)
 #define H9K_RARE __device__ __forceinline__
 #else
 #define H9K_RARE static __attribute__((noinline, cold))

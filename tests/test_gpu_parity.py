@@ -71,7 +71,7 @@ def test_config4_spinup_decades_carry_state():
     assert same_bits(d2["state"], exp["state"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "solo", "mixed"])
+@pytest.mark.parametrize("kernel", ["pair", "pair2", "solo", "mixed"])
 def test_config5_l10_matches_reference_golden(kernel, monkeypatch):
     """Config 5 (0.25 deg, L = 10, NS = 24, GROW) against the reference
     rebuilt with nsoil_layers_max = 10: every annual mean (NaN for the cell
@@ -226,11 +226,12 @@ def test_config4_full_grid_30_years_sampled_against_oracle():
         assert same_bits(got[k][sample], v), k
 
 
-@pytest.mark.parametrize("kernel", ["pair", "solo", "mixed"])
+@pytest.mark.parametrize("kernel", ["pair", "pair2", "solo", "mixed"])
 def test_config5_l10_quarter_degree_sample(kernel, monkeypatch):
-    """10 soil layers (config 5) on 0.25 deg cells, NS=24, GROW on, both
-    year kernels and the mixed launch (the default at L=10 is the pair kernel,
-    h9g.hip l10_kind), against the C restatement on 2,048 cells.  The
+    """10 soil layers (config 5) on 0.25 deg cells, NS=24, GROW on, the
+    year kernels (pair at 3 and at 2 waves per SIMD, solo) and the mixed
+    launch (h9g.hip l10_kind picks by shard size), against the C restatement
+    on 2,048 cells.  The
     restatement is itself pinned at L=10 to the reference's own L=10 build
     (oracle/_ref/h9ref_l10: SHARED.f90:294,300 set to 10/11) by the golden
     c5_l10_sample, which test_config5_l10_matches_reference_golden runs here."""

@@ -22,11 +22,11 @@ def main():
     from hybrid9_amd.shard import shard_slice
     gid = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)
     lat = synth.cell_lat(gid, synth.NX025, synth.NY025)
-    for world in (1, 2, 4, 8):
+    for world in [int(w) for w in os.environ.get("L10_WORLDS", "1,2,4,8").split(",")]:
         sl = shard_slice(gid.size, 0, world)
         g, la = gid[sl], lat[sl]
         row = [f"N={world} cells={g.size}"]
-        for k in ("pair", "solo", "mixed", "auto"):
+        for k in os.environ.get("L10_KINDS", "pair,pair2,solo,mixed,auto").split(","):
             if k == "auto":
                 os.environ.pop("H9G_KERNEL", None)
             else:
