@@ -193,3 +193,21 @@ def test_forcing_reader_netcdf4_chunk_layouts(tmp_path, chunk, filters, monkeypa
     row = np.arange(3 * NX + 2, 3 * NX + 9, dtype=np.int64)
     got = h.nc_forcing_read(paths, NX, NY, row, 0, nt)
     assert np.array_equal(got, np.stack([data[k].reshape(nt, -1)[:, row] for k in range(7)]))
+
+
+@pytest.mark.skipif(not Path("/opt/conda/include/hdf5.h").exists(), reason="no HDF5 in this image")
+def test_synthetic_pgf_files_round_trip(tmp_path):
+    """tools/pgf_synth.py (the files bench.py --forcing nc4 reads each step)
+    holds the bench's own synthetic forcing at the land cells: read back
+    through h9g_nc_forcing_read it is bit-equal to synth.make_forcing."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import pgf_synth
+    from hybrid9_amd import synth
+    nx, ny, nland = 24, 12, 90
+    paths = pgf_synth.write_year(tmp_path, 1903, 40, nx=nx, ny=ny, nland=nland)
+    assert [Path(p).name for p in paths] == [f"{v}_pgfv2.1_1901-1910.nc4" for v in h.PGF_VARS]
+    g = synth.land_cells(nx, ny, nland)
+    got = h.nc_forcing_read(paths, nx, ny, g, 0, 40)
+    exp = synth.make_forcing(g, synth.cell_lat(g, nx, ny), synth.year_day0(1903), 40)
+    assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
