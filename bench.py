@@ -287,7 +287,7 @@ class NcFed:
     region is not overlapped.  Every year reads the same file year (its
     days 0..nday-1), so only year 1 matches the device-generated run."""
 
-    def __init__(self, ctx, W, directory):
+    def __init__(self, ctx, W, directory, gid):
         sys.path.insert(0, str(ROOT / "tools"))
         import pgf_synth
         import hybrid9_amd as h
@@ -299,12 +299,9 @@ class NcFed:
         self.k = 0
         self.nx, self.ny = 720, 360
         # a synchronous read of one year, for the ingest rate alone
-        g = np.asarray(ctx._gid if hasattr(ctx, "_gid") else [], np.int64)
-        self.read_s = None
-        if g.size:
-            t = time.perf_counter()
-            h.nc_forcing_read(self.paths, self.nx, self.ny, g, 0, 365)
-            self.read_s = time.perf_counter() - t
+        t = time.perf_counter()
+        h.nc_forcing_read(self.paths, self.nx, self.ny, np.asarray(gid, np.int64), 0, 365)
+        self.read_s = time.perf_counter() - t
 
     def step(self, s):
         from hybrid9_amd import synth
@@ -474,8 +471,7 @@ def main():
     src_years = pl["slot_year"] if not args.host_fed else years[:nslots]
     nc_fed = None
     if args.forcing == "nc4":
-        ctx._gid = gid
-        nc_fed = NcFed(ctx, W, tempfile.mkdtemp(prefix="h9pgf_"))
+        nc_fed = NcFed(ctx, W, tempfile.mkdtemp(prefix="h9pgf_"), gid)
         pl = dict(pl, slot_of_step=[None] * (W + K))
     else:
         for slot, y in enumerate(src_years):       # forcing resident in HBM
