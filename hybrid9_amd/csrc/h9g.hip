@@ -131,9 +131,19 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane >= H9G_PLANES) return;
+  // lanes 0..43: 22 pairs; 44..63: spare lanes, which join the pairs only in
+  // the per-layer phases (Split2, hydrology_pair).  Spare lane 44 + j mirrors
+  // pair lane j mod (the wave's pair lanes): its LDS column and starting
+  // state, never stored to, so the substep code it runs masked-in stays
+  // ordinary; a pure function of the lane, so nothing about it is carried in
+  // registers.
+  const bool spare = lane >= H9G_PLANES;
   const int h = lane & 1;
-  const int slot = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * H9G_PCPW + (lane >> 1);
+  const int slot0 = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * H9G_PCPW;
+  const int ncol = min(H9G_PCPW, a.cend - slot0);
+  if (ncol <= 0) return;             // an empty wave
+  const int pl = spare ? (lane - H9G_PLANES) % (2 * ncol) : lane;
+  const int slot = slot0 + (pl >> 1);
   if (slot >= a.cend) return;        // both lanes of a pair leave together
   const int c = a.perm ? a.perm[slot] : slot;
   const int io = a.sorted_io ? slot : c;   // forcing and annual sums: slot order when sorted
@@ -141,24 +151,27 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
 
   int prow, pslot;
   pace_key(prow, pslot);
-  PS cs{(lds_float *)&s_cell[wave][lane], (lds_float *)&s_cell[wave][lane & ~1], (const lds_float *)s_zt,
+  PS cs{(lds_float *)&s_cell[wave][pl], (lds_float *)&s_cell[wave][pl & ~1], (const lds_float *)s_zt,
         a.sv + (size_t)blockIdx.x * (PS::GBLOCK / sizeof(float)),
         Pacer{a.pace + (size_t)prow * 16, a.epoch & 0xfffffu, pslot, a.prio_mode,
-              (int)((blockIdx.x * (unsigned)PS::RESIDENT) / gridDim.x)}};
-  const Split2 sp{h};
+              (int)((blockIdx.x * (unsigned)PS::RESIDENT) / gridDim.x)},
+        (lds_float *)&s_cell[wave][0]};
+  const Split2 sp{h, lane, spare};
   St<L> s;
+  if (!spare) {
 #pragma unroll
-  for (int p = 0; p < 4; p++)
+    for (int p = 0; p < 4; p++)
 #pragma unroll
-    for (int t = 0; t < L / 2; t++) cs.set_slot(p, t, a.par[(size_t)(p * L + 2 * t + h) * n + c]);
-  cs.set_sc(PS_FMAX, a.par[(size_t)(4 * L) * n + c]);
+      for (int t = 0; t < L / 2; t++) cs.set_slot(p, t, a.par[(size_t)(p * L + 2 * t + h) * n + c]);
+    cs.set_sc(PS_FMAX, a.par[(size_t)(4 * L) * n + c]);
+#pragma unroll
+    for (int t = 0; t < L / 2; t++) cs.set_slot(PF_ROOTR, t, a.st[(size_t)(3 * L + 2 * t + h) * n + c]);
+  }
 #pragma unroll
   for (int i = 1; i <= L; i++) {
     s.h2o[i] = a.st[(size_t)(0 * L + i - 1) * n + c];
     s.smp[i] = a.st[(size_t)(2 * L + i - 1) * n + c];
   }
-#pragma unroll
-  for (int t = 0; t < L / 2; t++) cs.set_slot(PF_ROOTR, t, a.st[(size_t)(3 * L + 2 * t + h) * n + c]);
   const size_t o8 = (size_t)(4 * L + 1) * n + c;
   s.zwt = a.st[o8 + 0 * (size_t)n];
   s.wa = a.st[o8 + 1 * (size_t)n];
@@ -170,17 +183,19 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   s.rdepth = a.st[o8 + 7 * (size_t)n];
   cs.launder();
 
-  // soil mask (HYBRID9.f90:122-123): SUM(theta_s) > trunc
-  float ts_sum = zero;
+  if (!spare) {
+    // soil mask (HYBRID9.f90:122-123): SUM(theta_s) > trunc
+    float ts_sum = zero;
 #pragma unroll
-  for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.lay(PF_TS, i);
-  if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
-    if (h == 0)
+    for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.lay(PF_TS, i);
+    if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
+      if (h == 0)
 #pragma unroll
-      for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + io] = __builtin_nanf("");
-    return;
+        for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + io] = __builtin_nanf("");
+      return;
+    }
+    cell_inv_pair<L, G>(g, cs);
   }
-  cell_inv_pair<L, G>(g, cs);
   int eday = 0, estep = 0;
   float errval = 0.0f;
 #if defined(H9G_STAMPS)
@@ -194,7 +209,7 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   const int code = cell_year_pair<L, G>(g, cs, sp, s, (const gbl_float *)(a.forc + io), (size_t)n, a.fvar, a.nt, a.nisurf,
                                         a.grow_on, (gbl_float *)(a.annual + io), (size_t)n, eday, estep, errval, T);
 #endif
-  if (h != 0) return;                // the even lane writes the cell back
+  if (spare || h != 0) return;       // the even lane writes the cell back
   int cw = c, iow = io;
   opaque(cw);
   opaque(iow);

@@ -113,6 +113,25 @@ H9K_HD float pair_bcast(float v) {
 #endif
 }
 
+// value of lane `src` of the wave (ds_bpermute: the LDS crossbar, no LDS
+// storage); the spare lanes' operands and results (hydrology_pair)
+H9K_HD float lane_get(float v, int src) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src << 2, __builtin_bit_cast(int, v)));
+#else
+  (void)src;
+  return v;
+#endif
+}
+H9K_HD int lane_geti(int v, int src) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ds_bpermute(src << 2, v);
+#else
+  (void)src;
+  return v;
+#endif
+}
+
 // A double kept as two float fields (low word, high word).
 H9K_HD double join_d(float lo, float hi) {
   return __builtin_bit_cast(double, (uint64_t)__builtin_bit_cast(uint32_t, hi) << 32 |
@@ -285,6 +304,8 @@ struct PairStore {
   // §3); the 2-wave build has the registers for H9G_FE2 slots per region
   static constexpr int FE_EQ = R <= 2 ? H9G_FE2 : H9G_FE_EQ, FE_HK = R <= 2 ? H9G_FE2 : H9G_FE_HK;
   Pacer pace;
+  lds_float *wb;                       // the wave's block (column 0): spare lanes' stolen slots
+  static constexpr int LANES = S;
   __device__ __forceinline__ void day_start(int day) const { pace.day_start(day, RESIDENT); }
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
@@ -453,6 +474,8 @@ struct StampProf {                     // wave-uniform shader-clock deltas per p
 // ---------------------------------------------------------------- policies
 // One lane computes every layer.
 struct SplitAll {
+  static constexpr bool kSpare = false;
+  H9K_HD constexpr bool act() const { return true; }
   H9K_HD SplitAll fresh() const { return *this; }
   template <class CS>
   H9K_HD float own(const CS &cs, int p, int t, int h) const { return cs.lay(p, 2 * t + 1 + h); }
@@ -502,11 +525,18 @@ struct SplitAll {
   H9K_HD double own_day_rp(const CS &cs, int j, int h) const { return cs.day_rp(j, h); }
 };
 
-// Two lanes per column (device fast path); h = lane & 1.
+// Two lanes per column (device fast path); h = lane & 1.  The wave's lanes
+// past the pairs (spare lanes, ln >= PairStore::LANES) take part only in the
+// per-layer phases, where they evaluate the pairs' last slot (hydrology_pair)
+// and are masked off everywhere else (act()).
 struct Split2 {
   int h;
+  int ln;                         // lane in the wave
+  bool spare;
+  static constexpr bool kSpare = true;
+  H9K_HD bool act() const { return !spare; }
   H9K_HD Split2 fresh() const {   // h, opaque to the optimiser (hydrology_pair)
-    Split2 r{h};
+    Split2 r{h, ln, spare};
     opaque(r.h);
     return r;
   }
@@ -913,16 +943,18 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
     // fast: the same values branch-free (all three cases evaluated, the
     // layer's selected); bad = some quotient or power of the selected case
     // needs its other path (then eq_exact recomputes the slot).  Bases of
-    // cases not taken are replaced by 1 so they raise no flag.
-    auto eq_fast = [&](int t, int h, bool &bad) __attribute__((always_inline)) -> FV<1> {
-          const int il = 2 * t + 1 + h;
+    // cases not taken are replaced by 1 so they raise no flag.  eq_body is
+    // the slot of layer il, with O(p) the slot's value of field p and zw the
+    // water table (mm): a lane's own slot (eq_fast) or, on a spare lane,
+    // another pair's last slot (below).
+    auto eq_body = [&](int il, auto O, float zw, bool &bad) __attribute__((always_inline)) -> FV<1> {
           const float zlo = cs.zi(il - 1), zhi = cs.zi(il);
-          const float ts = OWN(PF_TS), psi = OWN(PF_PSI);
-          const bool sat = zwtmm <= zlo;
-          const bool inl = (zwtmm < zhi) && (zwtmm > zlo);
-          const float expo = one + OWN(PF_NINVB);
-          auto rp = [&]() __attribute__((always_inline)) { return join_d(OWN(PF_RPSI0), OWN(PF_RPSI1)); };
-          const float n0 = ((-psi) + zwtmm - zlo), ni = (-psi + zwtmm - zhi);
+          const float ts = O(PF_TS), psi = O(PF_PSI);
+          const bool sat = zw <= zlo;
+          const bool inl = (zw < zhi) && (zw > zlo);
+          const float expo = one + O(PF_NINVB);
+          auto rp = [&]() __attribute__((always_inline)) { return join_d(O(PF_RPSI0), O(PF_RPSI1)); };
+          const float n0 = ((-psi) + zw - zlo), ni = (-psi + zw - zhi);
           float b0 = divr_d<CS::kRecip>(m, n0, -psi, rp, bad);
           float bi = divr_d<CS::kRecip>(m, ni, -psi, rp, bad);
           b0 = sat ? one : b0;
@@ -937,24 +969,27 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           float vin = zero;
           if (any_lane(inl)) {
           H9G_BR(BR_INL);
-          const float d0 = zwtmm - zlo;
-          const float q1 = m.div_d(OWN(PF_PTE), d0, recip64(d0));
+          const float d0 = zw - zlo;
+          const float q1 = m.div_d(O(PF_PTE), d0, recip64(d0));
           const float voleq1 = q1 * (one - temp0);
-          vin = m.div_d(voleq1 * (zwtmm - zlo) + ts * (zhi - zwtmm), zhi - zlo, cs.rdz_t(il));
+          vin = m.div_d(voleq1 * (zw - zlo) + ts * (zhi - zw), zhi - zlo, cs.rdz_t(il));
           bad |= inl && (m.div_bad(q1) | m.div_bad(vin));
           vin = MINF(ts, vin);
           vin = MAXF(vin, zero);
           }
           // water table below the layer (:548-558)
-          float vbl = OWN(PF_C3) * (tpi - temp0);
+          float vbl = O(PF_C3) * (tpi - temp0);
           vbl = MAXF(vbl, 0.0f);
           vbl = MINF(ts, vbl);
           const float vol_eq = sat ? ts : (inl ? vin : vbl);
-          const float qv = divr_d<CS::kRts>(m, vol_eq, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }, bad);
+          const float qv = divr_d<CS::kRts>(m, vol_eq, ts, [&]() { return join_d(O(PF_RTS0), O(PF_RTS1)); }, bad);
           bool sz;
-          const float z = psi * m.powf_d(MAXX(qv, 0.01f), -OWN(PF_BSW), sz);
+          const float z = psi * m.powf_d(MAXX(qv, 0.01f), -O(PF_BSW), sz);
           bad |= sz;
           return FV<1>{{MAXC(smpmin, z)}};
+    };
+    auto eq_fast = [&](int t, int h, bool &bad) __attribute__((always_inline)) -> FV<1> {
+          return eq_body(2 * t + 1 + h, [&](int p) __attribute__((always_inline)) { return OWN(p); }, zwtmm, bad);
     };
     auto hk_exact = [&](int t, int h) __attribute__((always_inline)) -> FV<4> {
           H9G_BR(BR_HKX);
@@ -989,29 +1024,26 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           r.v[3] = (-bsw) * sm / (s_node * ts);
           return r;
     };
-    // the same, branch-free, flags deferred (par_d)
-    auto hk_fast = [&](int t, int h, bool &bad) __attribute__((always_inline)) -> FV<4> {
-          const int i0 = 2 * t + 1;
-          const int ip1 = (L < i0 + 2) ? L : i0 + 2;
-          const float th = sel(h, theta[i0], theta[i0 + 1]);
-          const float thp = sel(h, theta[i0 + 1], theta[ip1]);
-          const float ts = OWN(PF_TS);
-          const float tsp = sel(h, TS(i0 + 1), TS(ip1));
+    // the same, branch-free, flags deferred (par_d); hk_body as eq_body, with
+    // the slot's operands theta(i), theta(ip), theta_s(ip) (ip = i + 1, at
+    // most L) given
+    auto hk_body = [&](auto O, float th, float thp, float tsp, bool &bad) __attribute__((always_inline)) -> FV<4> {
+          const float ts = O(PF_TS);
           // s1 = RN(0.5a / 0.5b) = RN(a / b) (the halvings are exact for
           // normal a, b), from y = PF_ITS = RN(1/b) by Markstein's correction:
           // q0 = RN(a y), e = a - b q0 (exact), RN(q0 + e y) = RN(a / b) when
           // nothing under- or overflows.  a, b in [2^-60, 2^60) keeps q and e
           // normal; other operands flag the slot for hk_exact.  (The IEEE
           // division took 11 VALU in a chain of 9; tools/markstein_check.c.)
-          const float sa = th + thp, sb = ts + tsp, its = OWN(PF_ITS);
+          const float sa = th + thp, sb = ts + tsp, its = O(PF_ITS);
           const float q0 = sa * its;
           float s1 = __builtin_fmaf(__builtin_fmaf(-sb, q0, sa), its, q0);
           const uint32_t ua = __builtin_bit_cast(uint32_t, sa) - 0x21800000u;   // 2^-60
           const uint32_t ub = __builtin_bit_cast(uint32_t, sb) - 0x21800000u;
           bad |= (ua > ub ? ua : ub) >= 0x5d800000u - 0x21800000u;             // 2^60
           s1 = MINC(one, s1);
-          const float bsw = OWN(PF_BSW);
-          float s_node = MAXX(divr_d<CS::kRtsHK>(m, th, ts, [&]() { return join_d(OWN(PF_RTS0), OWN(PF_RTS1)); }, bad),
+          const float bsw = O(PF_BSW);
+          float s_node = MAXX(divr_d<CS::kRtsHK>(m, th, ts, [&]() { return join_d(O(PF_RTS0), O(PF_RTS1)); }, bad),
                               0.01f);
           s_node = MINC(one, s_node);
           const float ek = 2.0f * bsw + 2.0f, es = -bsw;
@@ -1019,21 +1051,132 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           const float pk = m.powf_d(s1, ek, sk);
           const float ps = m.powf_d(s_node, es, ss);
           bad |= sk | ss;
-          const float s2 = OWN(PF_HKS) * pk;
+          const float s2 = O(PF_HKS) * pk;
           FV<4> r;
           r.v[0] = s1 * s2;
-          r.v[1] = (2.0f * bsw + 3.0f) * s2 * OWN(PF_ITS);
-          float sm = OWN(PF_PSI) * ps;
+          r.v[1] = (2.0f * bsw + 3.0f) * s2 * O(PF_ITS);
+          float sm = O(PF_PSI) * ps;
           sm = MAXC(smpmin, sm);
           r.v[2] = sm;
           r.v[3] = (-bsw) * sm / (s_node * ts);
           return r;
     };
-    // (round 3: the two phases' slots interleaved in one region, twice the
-    // independent powers per region, spilled 225 VGPRs: 214.5 vs 208.9 ms)
-    sp.template par_d<NT, 1, CS::FE_EQ>(eq_fast, eq_exact, outq);
-    pr.mark(2);
-    sp.template par_d<NT, 4, CS::FE_HK>(hk_fast, hk_exact, outk);
+    auto hk_fast = [&](int t, int h, bool &bad) __attribute__((always_inline)) -> FV<4> {
+          const int i0 = 2 * t + 1;
+          const int ip1 = (L < i0 + 2) ? L : i0 + 2;
+          return hk_body([&](int p) __attribute__((always_inline)) { return OWN(p); }, sel(h, theta[i0], theta[i0 + 1]),
+                         sel(h, theta[i0 + 1], theta[ip1]), sel(h, TS(i0 + 1), TS(ip1)), bad);
+    };
+    if constexpr (SP::kSpare && !M::kExact) {
+      // Spare lanes (round 4).  A wave's 22 pairs use 44 of its 64 lanes.  In
+      // these two phases -- a slot per round, NT rounds -- the 20 spare lanes
+      // evaluate the pairs' last slot (NT - 1) while the pairs do slots
+      // 0 .. NT - 2: in round q spare lane S + j takes pair lane k = j + 20q,
+      // with k's operands by ds_bpermute (all fetched before the first
+      // round) and its parameters from k's LDS column.  After the rounds pair
+      // lane k takes its result from spare lane S + k % 20 (round k / 20) and
+      // the flags of that evaluation with it.  NT - 1 rounds instead of NT,
+      // the same expressions on the same operands: no bit changes.  A flag on
+      // either side re-runs the pair lane's slots exactly, as in par_d.
+      constexpr int S = CS::LANES, NSP = 64 - S, QS = (S + NSP - 1) / NSP;   // QS: rounds with spare work
+      static_assert(QS <= NT - 1, "the spare lanes cover the last slot in NT - 1 rounds");
+      const bool st = sp.spare;
+      const int hh = sp.h;
+      auto kq = [&](int q) __attribute__((always_inline)) {   // spare lane: the pair lane of round q
+        const int k = sp.ln - S + NSP * (q < QS ? q : QS - 1);
+        return k < S - 1 ? k : S - 1;
+      };
+      const int qo = sp.ln / NSP, src = S + sp.ln % NSP;   // pair lane: round and spare lane of its last slot
+      auto back = [&](const float (&v)[NT - 1]) __attribute__((always_inline)) {
+        float x = lane_get(v[0], src);
+#pragma unroll
+        for (int q = 1; q < QS; q++) {
+          const float g = lane_get(v[q], src);
+          x = qo == q ? g : x;
+        }
+        return x;
+      };
+      {
+        float zwk[QS];
+#pragma unroll
+        for (int q = 0; q < QS; q++) zwk[q] = lane_get(zwtmm, kq(q));
+        FV<1> r[NT];
+        float rv[NT - 1];
+        int fl = 0;
+#pragma unroll
+        for (int q = 0; q < NT - 1; q++) {
+          const int k = kq(q);
+          const lds_float *o = st ? cs.wb + k + (NT - 1) * S : cs.self + q * S;
+          bool b = false;
+          r[q] = eq_body(st ? L - 1 + (k & 1) : 2 * q + 1 + hh,
+                         [&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
+                         st ? zwk[q < QS ? q : QS - 1] : zwtmm, b);
+          rv[q] = r[q].v[0];
+          fl |= (b ? 1 : 0) << q;
+          sched_fence();
+        }
+        r[NT - 1].v[0] = back(rv);
+        const int gf = lane_geti(fl, src);
+        const bool bad = !st & ((fl | ((gf >> qo) & 1)) != 0);
+        if (__builtin_expect(bad, 0)) {
+#pragma unroll
+          for (int t = 0; t < NT; t++) r[t] = eq_exact(t, hh);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; t++) sp.xchg(r[t].v[0], zq[2 * t + 1], zq[2 * t + 2]);
+      }
+      pr.mark(2);
+      {
+        const float th_l = sel(hh, theta[L - 1], theta[L]), thp_l = theta[L];   // this lane's last-slot operands
+        float thk[QS], thpk[QS];
+#pragma unroll
+        for (int q = 0; q < QS; q++) {
+          thk[q] = lane_get(th_l, kq(q));
+          thpk[q] = lane_get(thp_l, kq(q));
+        }
+        const lds_float *pe = cs.even + PF_TS * NT * S + (hh ? S : 1);           // TS(i + 1), TS(ip) of own slots
+        FV<4> r[NT];
+        int fl = 0;
+#pragma unroll
+        for (int q = 0; q < NT - 1; q++) {
+          const int k = kq(q), qq = q < QS ? q : QS - 1;
+          const lds_float *o = st ? cs.wb + k + (NT - 1) * S : cs.self + q * S;
+          const lds_float *pt = st ? cs.wb + (k | 1) + (PF_TS * NT + NT - 1) * S : pe + q * S;
+          bool b = false;
+          r[q] = hk_body([&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
+                         st ? thk[qq] : sel(hh, theta[2 * q + 1], theta[2 * q + 2]),
+                         st ? thpk[qq] : sel(hh, theta[2 * q + 2], theta[2 * q + 3]), *pt, b);
+          fl |= (b ? 1 : 0) << q;
+          sched_fence();
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+          float rv[NT - 1];
+#pragma unroll
+          for (int q = 0; q < NT - 1; q++) rv[q] = r[q].v[kk];
+          r[NT - 1].v[kk] = back(rv);
+        }
+        const int gf = lane_geti(fl, src);
+        const bool bad = !st & ((fl | ((gf >> qo) & 1)) != 0);
+        if (__builtin_expect(bad, 0)) {
+#pragma unroll
+          for (int t = 0; t < NT; t++) r[t] = hk_exact(t, hh);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+          for (int kk = 0; kk < 4; kk++) sp.xchg(r[t].v[kk], outk[kk][2 * t + 1], outk[kk][2 * t + 2]);
+      }
+    } else {
+      // (round 3: the two phases' slots interleaved in one region, twice the
+      // independent powers per region, spilled 225 VGPRs: 214.5 vs 208.9 ms)
+      sp.template par_d<NT, 1, CS::FE_EQ>(eq_fast, eq_exact, outq);
+      pr.mark(2);
+      sp.template par_d<NT, 4, CS::FE_HK>(hk_fast, hk_exact, outk);
+    }
+  }
+  if constexpr (SP::kSpare) {
+    if (!sp.act()) return 0;             // spare lanes: only the per-layer phases above
   }
   // First round of single powers, one per lane, chosen by where the lane's
   // water table is (jwt = L: below the column), with the lane's operands:
@@ -1650,9 +1793,9 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
   // test builds: also re-run every H9G_FORCE_RERUN-th substep of a day that
   // could (the exact replay from the day snapshot must reproduce the fast
   // path's state)
-  if (in_column && ns % H9G_FORCE_RERUN == H9G_FORCE_RERUN - 1) mf.special = true;
+  if (sp.act() && in_column && ns % H9G_FORCE_RERUN == H9G_FORCE_RERUN - 1) mf.special = true;
 #elif defined(H9G_FORCE_RERUN_ANY)
-  if (in_column && ns % H9G_FORCE_RERUN_ANY == H9G_FORCE_RERUN_ANY - 1) mf.special = true;
+  if (sp.act() && in_column && ns % H9G_FORCE_RERUN_ANY == H9G_FORCE_RERUN_ANY - 1) mf.special = true;
 #endif
   if (__builtin_expect(sp.pair_any(mf.special), 0)) {
     H9G_BR(BR_RERUN);
@@ -1692,12 +1835,18 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
   gbl_float *A = acc;
   const size_t as = astride;
   float rnf_sum = zero;
+  // spare lanes (Split2) run only the substeps' per-layer phases: everything
+  // here that stores is behind act()
+  const bool act = sp.act();
+  if (act) {
 #pragma unroll
-  for (int k = 0; k < 12 + L; k++) A[k * as] = zero;
+    for (int k = 0; k < 12 + L; k++) A[k * as] = zero;
+  }
   // plant state parked in the store over the substeps (read by day_consts
   // and GROW only, once a day)
   auto park = [&]() __attribute__((always_inline)) {
     if constexpr (Park) {
+      if (!act) return;
       cs.set_sc(PS_LAI, s.LAI);
       cs.set_sc(PS_LAIL, s.LAI_litter);
       cs.set_sc(PS_PM, s.pm);
@@ -1724,7 +1873,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
     opaque(A);
     const gbl_float *f = forc + (size_t)day * fday;
     opaque(f);
-    {
+    if (act) {
       float fv[7];             // tas rlds rsds huss ps pr rhs
 #pragma unroll
       for (int k = 0; k < 7; k++) fv[k] = ld_stream(f + k * fvar);
@@ -1751,7 +1900,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
       // layers (:923-1118), so only it can need the exact re-run
       const bool in_column = s.zwt <= g.zim(L);
       s.naq += in_column ? 0 : 1;
-      if (!snapped && in_column) {
+      if (act && !snapped && in_column) {
         H9G_BR(BR_SNAP);
         save_day<L>(sp, cs, s, rnf_sum, ns);
         snapped = true;
@@ -1769,6 +1918,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
       s.rdepth = cs.sc(PS_RDEPTH);
     }
     if (code) return code;
+    if (!act) continue;
     opaque(A);
     if (grow_on) {
       opaque(f);               // tas again (not kept live over the substeps)
@@ -1798,6 +1948,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
       if (later(k)) A[k * as] = a[k];
   }
   // :263-290
+  if (!act) return 0;
   opaque(A);
   A[A_PM * as] = A[A_PM * as] / (float)nt;
   A[A_RNF * as] = rnf_sum / (float)(nt * nisurf);
