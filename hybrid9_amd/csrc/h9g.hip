@@ -138,6 +138,7 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   // ordinary; a pure function of the lane, so nothing about it is carried in
   // registers.
   const bool spare = lane >= H9G_PLANES;
+  if (spare && !PS::kSpare) return;
   const int h = lane & 1;
   const int slot0 = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * H9G_PCPW;
   const int ncol = min(H9G_PCPW, a.cend - slot0);

@@ -81,6 +81,15 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
 #ifndef H9G_FE2
 #define H9G_FE2 1     // both, in the 2-wave build (PairStore R = 2)
 #endif
+#ifndef H9G_SPARE_PRE
+#define H9G_SPARE_PRE 1   // spare lanes' operands fetched before the rounds (hydrology_pair)
+#endif
+#ifndef H9G_SPARE_FENCE
+#define H9G_SPARE_FENCE 0      // rounds of the spare-lane phases followed by a scheduling fence (bit q)
+#endif
+#ifndef H9G_SPARE_L10
+#define H9G_SPARE_L10 0   // spare lanes in the 3-wave L = 10 build too (PairStore::kSpare)
+#endif
 
 template <int K>
 struct FV {
@@ -150,7 +159,7 @@ H9K_HD float hi_d(double v) {
 // kRts, kDayRecip say which reciprocal fields it holds (LDS budget).
 template <int L>
 struct FlatStore {                     // host: one flat array per cell
-  static constexpr bool kRecip = true, kRts = true, kDayRecip = true, kRtsHK = true;
+  static constexpr bool kRecip = true, kRts = true, kDayRecip = true, kRtsHK = true, kSpare = false;
   static constexpr int FE_EQ = 1, FE_HK = 1;
   static constexpr int N = PF_N * L + PS_N;
   float *b;
@@ -306,6 +315,9 @@ struct PairStore {
   Pacer pace;
   lds_float *wb;                       // the wave's block (column 0): spare lanes' stolen slots
   static constexpr int LANES = S;
+  // spare lanes in the per-layer phases (hydrology_pair): not in the 3-wave
+  // L = 10 build, whose registers they push further into scratch
+  static constexpr bool kSpare = H9G_SPARE_L10 || !(L >= 10 && R >= 3);
   __device__ __forceinline__ void day_start(int day) const { pace.day_start(day, RESIDENT); }
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
@@ -381,7 +393,7 @@ struct PairStore {
 // (1054 waves = 5 blocks/CU), day snapshot in LDS.
 template <int L>
 struct SoloStore {
-  static constexpr bool kRecip = false, kRts = false, kDayRecip = false, kRtsHK = false;
+  static constexpr bool kRecip = false, kRts = false, kDayRecip = false, kRtsHK = false, kSpare = false;
   static constexpr int FE_EQ = 1, FE_HK = 1;
   static constexpr int NPF = PF_RPSI0 + 2;           // TS..ROOTR, SVH2O, SVSMP
   static constexpr int NPS = PS_LAI + 5;             // FMAX..DAY, SV*
@@ -1067,7 +1079,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           return hk_body([&](int p) __attribute__((always_inline)) { return OWN(p); }, sel(h, theta[i0], theta[i0 + 1]),
                          sel(h, theta[i0 + 1], theta[ip1]), sel(h, TS(i0 + 1), TS(ip1)), bad);
     };
-    if constexpr (SP::kSpare && !M::kExact) {
+    if constexpr (SP::kSpare && CS::kSpare && !M::kExact) {
       // Spare lanes (round 4).  A wave's 22 pairs use 44 of its 64 lanes.  In
       // these two phases -- a slot per round, NT rounds -- the 20 spare lanes
       // evaluate the pairs' last slot (NT - 1) while the pairs do slots
@@ -1087,6 +1099,11 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
         return k < S - 1 ? k : S - 1;
       };
       const int qo = sp.ln / NSP, src = S + sp.ln % NSP;   // pair lane: round and spare lane of its last slot
+      // operands fetched before the rounds (latency off the rounds' path), or
+      // in each round (fewer live registers).  A ds_bpermute must run in
+      // converged control flow: a lane reads only what active lanes provide
+      // (a spare-lanes-only fetch under `st ?` read zeros: wrong results).
+      constexpr bool kPre = H9G_SPARE_PRE;
       auto back = [&](const float (&v)[NT - 1]) __attribute__((always_inline)) {
         float x = lane_get(v[0], src);
 #pragma unroll
@@ -1098,8 +1115,10 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
       };
       {
         float zwk[QS];
+        if constexpr (kPre) {
 #pragma unroll
-        for (int q = 0; q < QS; q++) zwk[q] = lane_get(zwtmm, kq(q));
+          for (int q = 0; q < QS; q++) zwk[q] = lane_get(zwtmm, kq(q));
+        }
         FV<1> r[NT];
         float rv[NT - 1];
         int fl = 0;
@@ -1107,13 +1126,14 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
         for (int q = 0; q < NT - 1; q++) {
           const int k = kq(q);
           const lds_float *o = st ? cs.wb + k + (NT - 1) * S : cs.self + q * S;
+          const float zwq = kPre ? zwk[q < QS ? q : QS - 1] : lane_get(zwtmm, k);   // in every lane (below)
           bool b = false;
           r[q] = eq_body(st ? L - 1 + (k & 1) : 2 * q + 1 + hh,
                          [&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
-                         st ? zwk[q < QS ? q : QS - 1] : zwtmm, b);
+                         st ? zwq : zwtmm, b);
           rv[q] = r[q].v[0];
           fl |= (b ? 1 : 0) << q;
-          sched_fence();
+          if ((H9G_SPARE_FENCE >> q) & 1) sched_fence();
         }
         r[NT - 1].v[0] = back(rv);
         const int gf = lane_geti(fl, src);
@@ -1129,10 +1149,12 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
       {
         const float th_l = sel(hh, theta[L - 1], theta[L]), thp_l = theta[L];   // this lane's last-slot operands
         float thk[QS], thpk[QS];
+        if constexpr (kPre) {
 #pragma unroll
-        for (int q = 0; q < QS; q++) {
-          thk[q] = lane_get(th_l, kq(q));
-          thpk[q] = lane_get(thp_l, kq(q));
+          for (int q = 0; q < QS; q++) {
+            thk[q] = lane_get(th_l, kq(q));
+            thpk[q] = lane_get(thp_l, kq(q));
+          }
         }
         const lds_float *pe = cs.even + PF_TS * NT * S + (hh ? S : 1);           // TS(i + 1), TS(ip) of own slots
         FV<4> r[NT];
@@ -1142,12 +1164,13 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           const int k = kq(q), qq = q < QS ? q : QS - 1;
           const lds_float *o = st ? cs.wb + k + (NT - 1) * S : cs.self + q * S;
           const lds_float *pt = st ? cs.wb + (k | 1) + (PF_TS * NT + NT - 1) * S : pe + q * S;
+          const float thq = kPre ? thk[qq] : lane_get(th_l, k), thpq = kPre ? thpk[qq] : lane_get(thp_l, k);
           bool b = false;
           r[q] = hk_body([&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
-                         st ? thk[qq] : sel(hh, theta[2 * q + 1], theta[2 * q + 2]),
-                         st ? thpk[qq] : sel(hh, theta[2 * q + 2], theta[2 * q + 3]), *pt, b);
+                         st ? thq : sel(hh, theta[2 * q + 1], theta[2 * q + 2]),
+                         st ? thpq : sel(hh, theta[2 * q + 2], theta[2 * q + 3]), *pt, b);
           fl |= (b ? 1 : 0) << q;
-          sched_fence();
+          if ((H9G_SPARE_FENCE >> q) & 1) sched_fence();
         }
 #pragma unroll
         for (int kk = 0; kk < 4; kk++) {
