@@ -133,17 +133,19 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // lanes 0..43: 22 pairs; 44..63: spare lanes, which join the pairs only in
   // the per-layer phases (Split2, hydrology_pair).  Spare lane 44 + j mirrors
-  // pair lane j mod (the wave's pair lanes): its LDS column and starting
-  // state, never stored to, so the substep code it runs masked-in stays
-  // ordinary; a pure function of the lane, so nothing about it is carried in
-  // registers.
+  // pair lane 12 + j (mod the wave's pair lanes): its LDS column and
+  // starting state, never stored to, so the substep code it runs masked-in
+  // stays ordinary; a pure function of the lane, so nothing about it is
+  // carried in registers.  Lanes 12..31 because an LDS read's lanes 32..63
+  // share one cycle (bank = dword mod 32): their columns' banks are the 20
+  // that pair lanes 32..43 leave free, so a mirrored read adds no conflict.
   const bool spare = lane >= H9G_PLANES;
   if (spare && !PS::kSpare) return;
   const int h = lane & 1;
   const int slot0 = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * H9G_PCPW;
   const int ncol = min(H9G_PCPW, a.cend - slot0);
   if (ncol <= 0) return;             // an empty wave
-  const int pl = spare ? (lane - H9G_PLANES) % (2 * ncol) : lane;
+  const int pl = spare ? (lane - H9G_PLANES + 12) % (2 * ncol) : lane;
   const int slot = slot0 + (pl >> 1);
   if (slot >= a.cend) return;        // both lanes of a pair leave together
   const int c = a.perm ? a.perm[slot] : slot;

@@ -273,6 +273,24 @@ def test_shard_invariance_and_determinism():
     assert same_bits(np.concatenate(parts, axis=2), ann_full)
 
 
+@pytest.mark.parametrize("L,nisurf,kernel", [(8, 48, "pair"), (10, 24, "pair2")])
+def test_spare_lanes_in_ragged_waves(L, nisurf, kernel, monkeypatch):
+    """The 20 spare lanes of a pair-kernel wave evaluate the pairs' last layer
+    slot and mirror pair lane j mod (the wave's pair lanes) elsewhere
+    (h9g.hip pair_body).  Waves with 1, 3, 9 and 22 + 1 columns (the mirror
+    wraps; a second, one-column wave) give the same bits for every cell as
+    the same cells inside a 1,500-cell run of full waves."""
+    monkeypatch.setenv("H9G_KERNEL", kernel)
+    gid = synth.land_cells()[::31][:1500]
+    ann_all, st_all, _ = _full_grid_gpu(gid, L, nisurf, True, 1901, 2)
+    for lo, n in ((0, 1), (5, 3), (101, 9), (700, 23)):
+        ann, st, _ = _full_grid_gpu(gid[lo:lo + n], L, nisurf, True, 1901, 2)
+        assert same_bits(ann, ann_all[:, :, lo:lo + n]), (lo, n)
+        part, full = refcase.unpack_state(st, n, L), refcase.unpack_state(st_all, gid.size, L)
+        for k in part:
+            assert same_bits(part[k], full[k][lo:lo + n]), (lo, n, k)
+
+
 @pytest.mark.parametrize("kernel", ["pair", "solo"])
 def test_cell_order_invariance(kernel, monkeypatch):
     """The per-year cell order (h9g_sort_kernel: keyed from year 2 on by the
