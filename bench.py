@@ -168,27 +168,27 @@ def cpu_baseline(workload: dict, seed: int) -> dict:
 
 def load_traffic(workload_name: str, kernel: str, build: str | None = None, root: Path = ROOT):
     """The PMC summary (profiles/pmc_<tag>.json, tools/prof.sh +
-    tools/pmc_summary.py) of this workload and kernel instantiation with the
-    latest tag, and whether it was measured on this build.  Returns
-    (summary, stale_tag): the summary only when its build_id equals `build`
-    (the loaded library's h9g_build_id), else (None, its tag) -- counters of
-    another build are never attached to this run's timing."""
+    tools/pmc_summary.py) of this workload and kernel instantiation measured
+    on this build (the loaded library's h9g_build_id; the latest such tag).
+    Returns (summary, None), or (None, stale_tag) with the latest tag of any
+    build when none matches -- counters of another build are never attached
+    to this run's timing."""
     def norm(k):
         k = k.replace("void ", "").replace("h9k::", "").replace(" ", "")
         return k.split("(")[0]
-    best = None
+    latest = match = None
     for p in sorted((root / "profiles").glob("pmc_*.json")):     # tags sort by round/version
         try:
             d = json.loads(p.read_text())
         except Exception:
             continue
         if d.get("workload") == workload_name and norm(d.get("kernel", "")) == norm(kernel):
-            best = d
-    if best is None:
-        return None, None
-    if build is None or best.get("build_id") != build:
-        return None, best.get("tag")
-    return best, None
+            latest = d
+            if build is not None and d.get("build_id") == build:
+                match = d
+    if match is not None:
+        return match, None
+    return None, (latest.get("tag") if latest is not None else None)
 
 
 def valu_roofline(pmc, launch_s: float):

@@ -150,9 +150,9 @@ def _pmc(root, tag, build, workload="config2", kernel="void h9g_pair_kernel<8, h
 
 
 def test_counters_attach_only_to_their_build(tmp_path):
-    """load_traffic attaches the latest summary of the workload and kernel
-    only if it was measured on this build (the r02f line cited
-    the r02e counters)."""
+    """load_traffic attaches a summary of the workload and kernel only if it
+    was measured on this build (the r02f line cited the r02e
+    counters), the latest such, whatever later tags of other builds exist."""
     k = "h9g_pair_kernel<8,GeoC<8,48>>"
     assert bench.load_traffic("config2", k, "aaaa", root=tmp_path) == (None, None)
     _pmc(tmp_path, "r03a", "aaaa")
@@ -160,8 +160,11 @@ def test_counters_attach_only_to_their_build(tmp_path):
     _pmc(tmp_path, "r03c", "aaaa", workload="config3")
     pmc, stale = bench.load_traffic("config2", k, "bbbb", root=tmp_path)
     assert stale is None and pmc["tag"] == "r03b"
-    # the latest config-2 summary is r03b: a library of build aaaa gets no counters
-    assert bench.load_traffic("config2", k, "aaaa", root=tmp_path) == (None, "r03b")
+    # build aaaa gets its own r03a counters, though r03b is later
+    pmc, stale = bench.load_traffic("config2", k, "aaaa", root=tmp_path)
+    assert stale is None and pmc["tag"] == "r03a"
+    # a build with no summary gets none, and the latest tag is reported
+    assert bench.load_traffic("config2", k, "cccc", root=tmp_path) == (None, "r03b")
     assert bench.load_traffic("config2", k, None, root=tmp_path) == (None, "r03b")
     assert bench.load_traffic("config3", k, "aaaa", root=tmp_path)[0]["tag"] == "r03c"
     assert bench.load_traffic("config2", "h9g_solo_kernel<8,GeoC<8,48>>", "bbbb", root=tmp_path) == (None, None)
