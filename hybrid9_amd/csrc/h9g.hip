@@ -199,6 +199,7 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
     }
     cell_inv_pair<L, G>(g, cs);
   }
+  if (__builtin_amdgcn_ballot_w64(!spare) == 0) return;   // every pair masked out: the spare lanes leave too
   int eday = 0, estep = 0;
   float errval = 0.0f;
 #if defined(H9G_STAMPS)

@@ -291,6 +291,24 @@ def test_spare_lanes_in_ragged_waves(L, nisurf, kernel, monkeypatch):
             assert same_bits(part[k], full[k][lo:lo + n]), (lo, n, k)
 
 
+def test_masked_waves_with_spare_lanes(monkeypatch):
+    """Cells outside the soil mask (SUM(theta_s) <= trunc, HYBRID9.f90:
+    122-123) leave the pair kernel at once; two whole waves of them (cells
+    0..43 in the identity cell order, H9G_SORT=0) leave their spare lanes
+    with no pair to serve, and those leave too.  The masked cells' annual
+    means are NaN, and every other cell is the reference's golden, bit for
+    bit."""
+    monkeypatch.setenv("H9G_KERNEL", "pair")
+    monkeypatch.setenv("H9G_SORT", "0")
+    meta, inp, exp = load_golden("c1_10x10")
+    p = {k: v.copy() for k, v in inp["params"].items()}
+    p["theta_s"][:44] = 0.0
+    out = h.run(zi=inp["zi"], params=p, forcing=inp["forcing"], nisurf=inp["nisurf"], year0=inp["year0"],
+                nyears=inp["nyears"], grow_on=bool(inp["grow_on"]), state0=inp["state0"], stop_on_error=False)
+    assert np.isnan(out["annual"][:, :, :44]).all()
+    assert same_bits(out["annual"][:, :, 44:], exp["annual"][:, :, 44:])
+
+
 @pytest.mark.parametrize("kernel", ["pair", "solo"])
 def test_cell_order_invariance(kernel, monkeypatch):
     """The per-year cell order (h9g_sort_kernel: keyed from year 2 on by the
