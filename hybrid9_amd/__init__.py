@@ -102,6 +102,8 @@ def lib() -> C.CDLL:
         "h9g_host_alloc": (vp, [C.c_size_t]),
         "h9g_host_free": (None, [vp]),
         "h9g_run_year": (C.c_int, [vp, C.c_int, C.c_int]),
+        "h9g_run_decade_ordered": (C.c_int, [vp, C.POINTER(C.c_int32), C.c_int, C.c_int, _FP,
+                                             C.POINTER(C.c_int32)]),
         "h9g_sync": (C.c_int, [vp]),
         "h9g_last_error": (C.c_int, [vp, C.POINTER(_Error)]),
         "h9g_get_errors": (C.c_int, [vp, C.POINTER(C.c_int32)]),
@@ -339,6 +341,21 @@ class Context:
     def run_year(self, slot: int, jyear: int):
         _check(self._lib.h9g_run_year(self._h, slot, jyear), "h9g_run_year")
 
+    def run_decade_ordered(self, slots, jyear0: int, raise_on_stop: bool = True):
+        """One decade of the reference's own cell order (h9g_run_decade_ordered:
+        smp carried from cell to cell, HYBRID9.f90:93-130); synchronous.
+        Returns (annual (nyears, 12+L, ncell), passes); self.decade_rc holds
+        the STOP code."""
+        sl = np.ascontiguousarray(slots, dtype=np.int32)
+        out = np.empty((sl.size, 12 + self.L, self.ncell), dtype=np.float32)
+        np_ = C.c_int32(0)
+        rc = _check(self._lib.h9g_run_decade_ordered(self._h, sl.ctypes.data_as(C.POINTER(C.c_int32)), jyear0,
+                                                     sl.size, _fp(out), C.byref(np_)), "h9g_run_decade_ordered")
+        self.decade_rc = rc
+        if rc and raise_on_stop:
+            raise ReferenceStop(self.last_error())
+        return out, int(np_.value)
+
     def run_site(self, sub, daily, lai, raise_on_stop: bool = True) -> np.ndarray:
         """LCLIM site path (HYBRID9.f90:339-480) over nday days, synchronous.
 
@@ -450,6 +467,48 @@ def write_axy_nc(path, annual, gid, zc, nx: int = 720, ny: int = 360):
     assert annual.shape[1] == gid.size and zc.size == L
     _check(lib().h9g_write_axy_nc(str(path).encode(), nx, ny, L, _fp(zc), gid.size,
                                   gid.ctypes.data_as(_I64P), _fp(annual)), "h9g_write_axy_nc")
+
+
+def decades(year0: int, nyears: int):
+    """The reference's decades (HYBRID9.f90:93-113: 1901-1910, 1911-1920,
+    ...) cut to [year0, year0 + nyears): list of (first year, years)."""
+    out, y, end = [], year0, year0 + nyears
+    while y < end:
+        e = min(1901 + 10 * ((y - 1901) // 10) + 10, end)
+        out.append((y, e - y))
+        y = e
+    return out
+
+
+def run_cell_order(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=True,
+                   state0: np.ndarray | None = None, device=0):
+    """``run`` in the reference's own cell order: decade by decade through
+    ``Context.run_decade_ordered`` (smp carried from cell to cell, cells in
+    the given order).  Returns dict(annual, state, rc, err, errors, passes
+    (per decade))."""
+    L = params["theta_s"].shape[1]
+    n = params["fmax"].size
+    with Context(n, zi, nlayers=L, nisurf=nisurf, grow_on=grow_on, device=device, nslots=10) as ctx:
+        ctx.set_params(params)
+        if state0 is None:
+            ctx.init_state()
+        else:
+            ctx.set_state(state0)
+        ann = np.full((nyears, 12 + L, n), np.nan, dtype=np.float32)
+        d0, rc, err, passes = 0, 0, None, []
+        for y0, ny in decades(year0, nyears):
+            for k in range(ny):
+                nt = days_in_year(y0 + k)
+                ctx.push_forcing(k, forcing[:, d0:d0 + nt, :])
+                d0 += nt
+            a, p = ctx.run_decade_ordered(list(range(ny)), y0, raise_on_stop=False)
+            ann[y0 - year0:y0 - year0 + ny] = a
+            passes.append(p)
+            rc = ctx.decade_rc
+            if rc:
+                err = ctx.last_error()
+                break
+        return dict(annual=ann, state=ctx.get_state(), rc=rc, err=err, errors=ctx.get_errors(), passes=passes)
 
 
 def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=True,

@@ -388,13 +388,54 @@ static unsigned perm_forcing_blocks(int c0, int cend, int cpb, int nt) {
   return H9G_NXCD * cmax * ((7u * (unsigned)nt + H9G_PF_ROWS - 1) / H9G_PF_ROWS);
 }
 
-// The annual sums of a sorted year kernel (slot order) back to cell order.
-__global__ void __launch_bounds__(256) h9g_unperm_annual_kernel(int n, int rows, const int *__restrict__ perm,
+// The annual sums of a sorted year kernel (slot order) back to cell order:
+// the m slots of the launch, rows of stride n.
+__global__ void __launch_bounds__(256) h9g_unperm_annual_kernel(int m, int n, int rows, const int *__restrict__ perm,
                                                                 const float *__restrict__ src, float *__restrict__ dst) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
+  if (s >= m) return;
   const int c = perm[s];
   for (int r = blockIdx.y; r < rows; r += gridDim.y) dst[(size_t)r * n + c] = src[(size_t)r * n + s];
+}
+
+// Cell-order mode (h9g_run_decade_ordered).  The reference's cell loop
+// (HYBRID9.f90:120-295) leaves the module array smp (SHARED.f90:198) as the
+// last cell's, and the next cell's first substep reads it in beta
+// (HYDROLOGY.f90:270-275).  Chain position j of m land cells (context
+// order) starts a decade from the smp cell chain[j-1] holds now (for j = 0:
+// what chain[m-1] held when the decade started).  h9g_chain_kernel compares
+// that with the smp the cell last started from (guess, L rows of n), takes
+// it over where it differs and flags the cell for a re-run.
+__global__ void __launch_bounds__(256) h9g_chain_kernel(int m, int n, int L, const int *__restrict__ chain,
+                                                        const float *__restrict__ st, const float *__restrict__ st0,
+                                                        float *__restrict__ guess, int *__restrict__ flag) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const int k = chain[j];
+  const float *src = j == 0 ? st0 : st;
+  const int p = j == 0 ? chain[m - 1] : chain[j - 1];
+  int differ = 0;
+  for (int i = 0; i < L; i++) {
+    const float v = src[(size_t)(2 * L + i) * n + p];
+    differ |= __float_as_uint(v) != __float_as_uint(guess[(size_t)i * n + k]);
+    guess[(size_t)i * n + k] = v;
+  }
+  flag[j] = differ;
+}
+
+// The listed cells back to the decade's starting state (state rows and STOP
+// record), starting from the smp in guess.
+__global__ void __launch_bounds__(256) h9g_restart_kernel(int m, int n, int L, const int *__restrict__ list,
+                                                          const float *__restrict__ st0, const int *__restrict__ err0,
+                                                          const float *__restrict__ guess, float *__restrict__ st,
+                                                          int *__restrict__ err) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const int k = list[j];
+  const int rows = 4 * L + 9;
+  for (int r = 0; r < rows; r++) st[(size_t)r * n + k] = st0[(size_t)r * n + k];
+  for (int i = 0; i < L; i++) st[(size_t)(2 * L + i) * n + k] = guess[(size_t)i * n + k];
+  for (int r = 0; r < 4; r++) err[(size_t)r * n + k] = err0[(size_t)r * n + k];
 }
 
 // Cell order of the next year kernel: a stable counting sort of the cells
@@ -1399,9 +1440,16 @@ static int pace_mode(const h9g_ctx *ctx, size_t m) {
   return blocks <= (size_t)ctx->ncu * resident ? 2 : 1;
 }
 
-int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
+// One year launch.  d_list == nullptr: every cell of the context, in the
+// order of h9g_sort_kernel (h9g_run_year).  Otherwise the m cells d_list[0..m)
+// in that order (the cell-order mode's re-runs, h9g_run_decade_ordered),
+// their annual means to ann_dst (rows of stride n, cell order).
+static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, int m, float *ann_dst) {
   if (!ctx || slot < 0 || slot >= ctx->cfg.nslots || jyear < 1861 || jyear > 2299) return H9G_EINVAL;
   if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
+#if defined(H9G_DUMP_AQ)
+  if (d_list) return H9G_EINVAL;
+#endif
   if (const int prc = join_prefetch(ctx, slot)) return prc;
   const int nt = days_in_year(jyear);
   if (ctx->slot_days[slot] < nt) return H9G_EINVAL;
@@ -1410,7 +1458,7 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   KArgs a;
   a.ncell = (int)ctx->n;
   a.c0 = 0;
-  a.cend = (int)ctx->n;
+  a.cend = d_list ? m : (int)ctx->n;
   a.nt = nt;
   a.nisurf = ctx->cfg.nisurf;
   a.grow_on = ctx->cfg.grow_on;
@@ -1426,7 +1474,22 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   a.perm = nullptr;
   a.sorted_io = 0;
   a.hist = ctx->d_hist;
-  if (ctx->sort) {             // per launch range and its workgroup size (h9g_sort_kernel)
+  // the launch's kernel: a list runs on the pair kernel (or the one the
+  // context's shard size chose at L = 10), never split into solo rounds
+  const int kind = d_list ? (ctx->kind == 3 ? 1 : ctx->kind) : ctx->kind;
+  const size_t ncells = d_list ? (size_t)m : ctx->n;
+  if (d_list) {
+    const int pcpb = kind == 2 ? H9G_YBLOCK : H9G_PCPW * H9G_PWAVES;
+    if (!ctx->d_forc_s) HIPCHK(hipMalloc(&ctx->d_forc_s, sizeof(float) * 7 * (size_t)ctx->cfg.max_days * ctx->n));
+    if (!ctx->d_ann_s) HIPCHK(hipMalloc(&ctx->d_ann_s, sizeof(float) * (12 + ctx->L) * ctx->n));
+    a.perm = d_list;
+    h9g_perm_forcing_kernel<<<perm_forcing_blocks(0, m, pcpb, nt), 256, 0, ctx->sc>>>(
+        0, m, pcpb, nt, (int)ctx->n, a.fvar, d_list, a.forc, ctx->d_forc_s);
+    HIPCHK(hipGetLastError());
+    a.forc = ctx->d_forc_s;
+    a.annual = ctx->d_ann_s;
+    a.sorted_io = 1;
+  } else if (ctx->sort) {             // per launch range and its workgroup size (h9g_sort_kernel)
     const int n = (int)ctx->n, ns = (int)ctx->n_solo, pcpb = H9G_PCPW * H9G_PWAVES;
     if (ctx->kind == 2) {
       H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, n, H9G_YBLOCK, ctx->d_st, ctx->d_err,
@@ -1467,7 +1530,7 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
     a.sorted_io = 1;
 #endif
   }
-  if (ctx->kind != 2) {
+  if (kind != 2) {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     const size_t need = ((ctx->n + per_block - 1) / per_block) * 65536;
     if (ctx->sv_bytes < need) {
@@ -1486,7 +1549,7 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
   }
   a.pace = ctx->d_pace;
   a.epoch = ++ctx->epoch;
-  a.prio_mode = pace_mode(ctx, ctx->kind == 3 ? ctx->n - ctx->n_solo : ctx->n);
+  a.prio_mode = pace_mode(ctx, kind == 3 ? ctx->n - ctx->n_solo : ncells);
 #if defined(H9G_STAMPS)
   if (!ctx->d_stamps) HIPCHK(hipMalloc(&ctx->d_stamps, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8)));
   HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8), ctx->sc));
@@ -1527,10 +1590,10 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
 #endif
   const int e = ctx->nev++;
   HIPCHK(hipEventRecord(ctx->ev0[e], ctx->sc));
-  if (ctx->kind == 2) {
-    H9G_DISPATCH(ctx, h9g_solo_kernel, (unsigned)((ctx->n + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
+  if (kind == 2) {
+    H9G_DISPATCH(ctx, h9g_solo_kernel, (unsigned)((ncells + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
                  ctx->sc, a);
-  } else if (ctx->kind == 3) {
+  } else if (kind == 3) {
     // mixed (l10_kind): whole rounds of solo waves, then the pair kernel on the rest
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     const size_t ns = ctx->n_solo;
@@ -1546,29 +1609,185 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
       H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n - ns + per_block - 1) / per_block), 64 * H9G_PWAVES,
                    ctx->sc, a);
     }
-  } else if (ctx->kind == 4) {
+  } else if (kind == 4) {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
-    H9G_DISPATCH_L10(ctx, h9g_pair2_kernel, (unsigned)((ctx->n + per_block - 1) / per_block), 64 * H9G_PWAVES,
+    H9G_DISPATCH_L10(ctx, h9g_pair2_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
                      ctx->sc, a);
   } else {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
-    H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n + per_block - 1) / per_block), 64 * H9G_PWAVES,
+    H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
                  ctx->sc, a);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1[e], ctx->sc));
   HIPCHK(hipEventRecord(ctx->ev_consumed[slot], ctx->sc));
   if (a.sorted_io) {
-    h9g_unperm_annual_kernel<<<dim3((unsigned)((ctx->n + 255) / 256), (unsigned)(12 + ctx->L)), 256, 0, ctx->sc>>>(
-        (int)ctx->n, 12 + ctx->L, ctx->d_perm, ctx->d_ann_s, ctx->d_ann);
+    h9g_unperm_annual_kernel<<<dim3((unsigned)((ncells + 255) / 256), (unsigned)(12 + ctx->L)), 256, 0, ctx->sc>>>(
+        (int)ncells, (int)ctx->n, 12 + ctx->L, a.perm, ctx->d_ann_s, d_list ? ann_dst : ctx->d_ann);
     HIPCHK(hipGetLastError());
   }
-  h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)ctx->n, ctx->L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
-  HIPCHK(hipGetLastError());
+  if (!d_list) {
+    h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)ctx->n, ctx->L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
+    HIPCHK(hipGetLastError());
+  }
   ctx->last_year = jyear;
   ctx->hist_nsub = nt * ctx->cfg.nisurf;
   ctx->ran = 1;
   return 0;
+}
+
+int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) { return run_year_impl(ctx, slot, jyear, nullptr, 0, nullptr); }
+
+// The reference's own cell order over one decade (include/h9g.h).  Pass 0
+// runs every cell from its own smp, except the chain's first cell, whose
+// input is known.  Each further pass gives every land cell the smp its
+// predecessor now leaves behind (h9g_chain_kernel) and re-runs the decade
+// for the cells whose input changed, from the decade's starting state.  A
+// cell's result depends on its predecessor's only through that smp, so when
+// no input changes every cell has run from the input the reference gives
+// it.  The chain's first cell never changes after pass 0, so pass p fixes
+// at least chain position p: at most m passes.
+int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int nyears, float *annual, int32_t *passes) {
+  if (!ctx || !slots || nyears < 1 || nyears > ctx->cfg.nslots) return H9G_EINVAL;
+  if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
+  for (int y = 0; y < nyears; y++)
+    if (slots[y] < 0 || slots[y] >= ctx->cfg.nslots || jyear0 + y < 1861 || jyear0 + y > 2299) return H9G_EINVAL;
+  const size_t n = ctx->n;
+  const int L = ctx->L, rows = 12 + L;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  // the chain: land cells (HYBRID9.f90:122-123, summed in layer order as the
+  // year kernels do) that have not stopped, in context order
+  std::vector<float> ts((size_t)L * n);
+  std::vector<int> err0h(n);
+  HIPCHK(hipMemcpy(ts.data(), ctx->d_par, sizeof(float) * ts.size(), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(err0h.data(), ctx->d_err, sizeof(int) * n, hipMemcpyDeviceToHost));
+  std::vector<int> chain;
+  for (size_t c = 0; c < n; c++) {
+    float sum = 0.0f;
+    for (int i = 0; i < L; i++) sum = sum + ts[(size_t)i * n + c];
+    if (sum > 1.0E-8f && err0h[c] == 0) chain.push_back((int)c);
+  }
+  const int m = (int)chain.size();
+  const size_t srows = (size_t)h9g_state_size(L);
+  float *d_st0 = nullptr, *d_guess = nullptr, *d_ann_dec = nullptr;
+  int *d_err0 = nullptr, *d_chain = nullptr, *d_list = nullptr, *d_flag = nullptr;
+  int rc = 0, np = 0;
+  auto fail = [&](int code) { rc = code; };
+  do {
+    if (hipMalloc(&d_st0, sizeof(float) * srows * n) != hipSuccess ||
+        hipMalloc(&d_guess, sizeof(float) * (size_t)L * n) != hipSuccess ||
+        hipMalloc(&d_ann_dec, sizeof(float) * (size_t)nyears * rows * n) != hipSuccess ||
+        hipMalloc(&d_err0, sizeof(int) * 4 * n) != hipSuccess || hipMalloc(&d_chain, sizeof(int) * (m + 1)) != hipSuccess ||
+        hipMalloc(&d_list, sizeof(int) * (m + 1)) != hipSuccess || hipMalloc(&d_flag, sizeof(int) * (m + 1)) != hipSuccess) {
+      fail(H9G_ENOMEM);
+      break;
+    }
+    if (hipMemcpyAsync(d_st0, ctx->d_st, sizeof(float) * srows * n, hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
+        hipMemcpyAsync(d_err0, ctx->d_err, sizeof(int) * 4 * n, hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
+        hipMemcpyAsync(d_guess, ctx->d_st + (size_t)2 * L * n, sizeof(float) * (size_t)L * n, hipMemcpyDeviceToDevice,
+                       ctx->sc) != hipSuccess) {
+      fail(H9G_EHIP);
+      break;
+    }
+    if (m > 0) {
+      if (hipMemcpy(d_chain, chain.data(), sizeof(int) * m, hipMemcpyHostToDevice) != hipSuccess) {
+        fail(H9G_EHIP);
+        break;
+      }
+      // pass 0's input of the chain's first cell: what the last one holds now
+      for (int i = 0; i < L; i++)
+        if (hipMemcpyAsync(ctx->d_st + (size_t)(2 * L + i) * n + chain[0], d_st0 + (size_t)(2 * L + i) * n + chain[m - 1],
+                           sizeof(float), hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
+            hipMemcpyAsync(d_guess + (size_t)i * n + chain[0], d_st0 + (size_t)(2 * L + i) * n + chain[m - 1],
+                           sizeof(float), hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess) {
+          fail(H9G_EHIP);
+          break;
+        }
+      if (rc) break;
+    }
+    for (int y = 0; y < nyears && !rc; y++) {   // pass 0: every cell
+      if (int r = run_year_impl(ctx, slots[y], jyear0 + y, nullptr, 0, nullptr)) {
+        fail(r);
+        break;
+      }
+      if (hipMemcpyAsync(d_ann_dec + (size_t)y * rows * n, ctx->d_ann, sizeof(float) * rows * n,
+                         hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess)
+        fail(H9G_EHIP);
+    }
+    if (rc) break;
+    np = 1;
+    std::vector<int> flag(m), list;
+    while (m > 0) {
+      h9g_chain_kernel<<<(unsigned)((m + 255) / 256), 256, 0, ctx->sc>>>(m, (int)n, L, d_chain, ctx->d_st, d_st0, d_guess,
+                                                                        d_flag);
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(flag.data(), d_flag, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->sc) != hipSuccess ||
+          hipStreamSynchronize(ctx->sc) != hipSuccess) {
+        fail(H9G_EHIP);
+        break;
+      }
+      list.clear();
+      for (int j = 0; j < m; j++)
+        if (flag[j]) list.push_back(chain[j]);
+      if (list.empty()) break;
+      if (np > m) {                 // cannot happen (see above): a broken invariant, not a result
+        fail(H9G_ESTATE);
+        break;
+      }
+      const int k = (int)list.size();
+      if (hipMemcpy(d_list, list.data(), sizeof(int) * k, hipMemcpyHostToDevice) != hipSuccess) {
+        fail(H9G_EHIP);
+        break;
+      }
+      h9g_restart_kernel<<<(unsigned)((k + 255) / 256), 256, 0, ctx->sc>>>(k, (int)n, L, d_list, d_st0, d_err0, d_guess,
+                                                                          ctx->d_st, ctx->d_err);
+      if (hipGetLastError() != hipSuccess) {
+        fail(H9G_EHIP);
+        break;
+      }
+      for (int y = 0; y < nyears && !rc; y++)
+        if (int r = run_year_impl(ctx, slots[y], jyear0 + y, d_list, k, d_ann_dec + (size_t)y * rows * n)) fail(r);
+      np++;
+    }
+    if (rc) break;
+    // the last year's means stay the context's annual output; diagnostics
+    if (hipMemcpyAsync(ctx->d_ann, d_ann_dec + (size_t)(nyears - 1) * rows * n, sizeof(float) * rows * n,
+                       hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess) {
+      fail(H9G_EHIP);
+      break;
+    }
+    h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)n, L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
+    if (hipGetLastError() != hipSuccess ||
+        (annual && hipMemcpyAsync(annual, d_ann_dec, sizeof(float) * (size_t)nyears * rows * n, hipMemcpyDeviceToHost,
+                                  ctx->sc) != hipSuccess))
+      fail(H9G_EHIP);
+  } while (0);
+  int src = 0;
+  if (!rc) {
+    const int had = ctx->last_err.code;
+    src = h9g_sync(ctx);   // folds the timings; the STOP of the first failing cell in context order
+    if (src > 0 && !had && ctx->last_err.cell >= 0) {
+      // its year: the first of the decade whose means it has not completed
+      std::vector<float> npp(nyears);
+      for (int y = 0; y < nyears; y++)
+        (void)hipMemcpy(&npp[y], d_ann_dec + (size_t)y * rows * n + ctx->last_err.cell, sizeof(float),
+                        hipMemcpyDeviceToHost);
+      int y = 0;
+      while (y < nyears - 1 && npp[y] == npp[y]) y++;
+      ctx->last_err.year = jyear0 + y;
+    }
+  }
+  (void)hipStreamSynchronize(ctx->sc);
+  (void)hipFree(d_st0);
+  (void)hipFree(d_guess);
+  (void)hipFree(d_ann_dec);
+  (void)hipFree(d_err0);
+  (void)hipFree(d_chain);
+  (void)hipFree(d_list);
+  (void)hipFree(d_flag);
+  if (passes) *passes = np;
+  return rc ? rc : src;
 }
 
 int h9g_sync(h9g_ctx *ctx) {

@@ -162,6 +162,19 @@ INTERFACE
     INTEGER(C_INT32_T), INTENT(OUT) :: rec (*)
     INTEGER(C_INT) :: h9g_get_errors
   END FUNCTION
+  ! The reference's cell order over one decade (HYBRID9.f90:93-130: smp
+  ! carried from cell to cell); annual (ncell, 12+L, nyears) in C order
+  ! (nyears, 12+L, ncell).
+  FUNCTION h9g_run_decade_ordered (ctx, slots, jyear0, nyears, annual, passes) &
+           BIND(C, NAME='h9g_run_decade_ordered')
+    IMPORT :: C_PTR, C_INT, C_INT32_T, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT32_T), INTENT(IN) :: slots (*)
+    INTEGER(C_INT), VALUE :: jyear0, nyears
+    REAL(C_FLOAT), INTENT(OUT) :: annual (*)
+    INTEGER(C_INT32_T), INTENT(OUT) :: passes
+    INTEGER(C_INT) :: h9g_run_decade_ordered
+  END FUNCTION
   FUNCTION h9g_get_diagnostics_async (ctx, dev_out, stream) &
            BIND(C, NAME='h9g_get_diagnostics_async')
     IMPORT :: C_PTR, C_INT

@@ -100,6 +100,70 @@ def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=1,
     return out
 
 
+def decades(year0, nyears):
+    """The reference's decades (HYBRID9.f90:93-113: 1901-1910, 1911-1920,
+    ...) cut to [year0, year0 + nyears): list of (first year, years)."""
+    out, y, end = [], year0, year0 + nyears
+    while y < end:
+        e = min(1901 + 10 * ((y - 1901) // 10) + 10, end)
+        out.append((y, e - y))
+        y = e
+    return out
+
+
+def run_cell_order(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=1,
+                   state0=None):
+    """The reference's own order (HYBRID9.f90:93-130): decade -> cell ->
+    year, with smp (SHARED.f90:198) carried from cell to cell: a land cell's
+    first substep of a decade reads the smp its predecessor in cell order
+    left behind (HYDROLOGY.f90:270-275); the first land cell reads the smp
+    the last land cell holds when the decade starts.  Restated on the C
+    oracle one (cell, decade) at a time; same contract as run()."""
+    L = params["theta_s"].shape[1]
+    n = params["fmax"].size
+    fo = np.ascontiguousarray(forcing, dtype=np.float32)
+    st = refcase.unpack_state(init_state(params, zi) if state0 is None
+                              else refcase.pack_state(state0, L), n, L)
+    st = {k: np.array(v, copy=True) for k, v in st.items()}
+    ann = np.full((nyears, 12 + L, n), np.nan, dtype=np.float32)
+    # the soil mask (HYBRID9.f90:122-123), summed in layer order
+    land =[c for c in range(n) if _mask_sum(params["theta_s"][c]) > np.float32(1.0e-8)]
+    one = lambda a, c: a[c:c + 1]  # noqa: E731
+    rc, err = 0, dict(code=0, cell=-1, day=-1, substep=-1, value=0.0)
+    day0 = 0
+    for y0, ny in decades(year0, nyears):
+        nd = sum(_days(y0 + k) for k in range(ny))
+        carry = st["smp"][land[-1]].copy() if land else None
+        for c in land:
+            s1 = {k: one(v, c).copy() for k, v in st.items()}
+            s1["smp"][0] = carry
+            r = run(zi=zi, params={k: one(v, c) for k, v in params.items()},
+                    forcing=np.ascontiguousarray(fo[:, day0:day0 + nd, c:c + 1]), nisurf=nisurf,
+                    year0=y0, nyears=ny, grow_on=grow_on, state0=s1)
+            for k in st:
+                st[k][c] = r["state"][k][0]
+            ann[y0 - year0:y0 - year0 + ny, :, c] = r["annual"][:, :, 0]
+            carry = st["smp"][c].copy()
+            if r["rc"] and not rc:
+                rc = r["rc"]
+                err = dict(r["err"], cell=c)
+        day0 += nd
+        if rc:
+            break
+    return dict(annual=ann, state=st, rc=rc, err=err)
+
+
+def _mask_sum(ts):
+    s = np.float32(0.0)
+    for v in ts:
+        s = np.float32(s + np.float32(v))
+    return s
+
+
+def _days(y):
+    return 365 if y % 4 else (366 if y % 100 else (365 if y % 400 else 366))
+
+
 def site(*, zi, params, sub, daily, lai, nisurf=48, state0=None, nthreads=1):
     """LCLIM site path restated (h9o_site); same contract as
     refcase.run_site_case; returns dict(daily, state, rc, err).  Masked and

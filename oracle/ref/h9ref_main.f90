@@ -22,6 +22,17 @@ PROGRAM H9REF
 !   * grow_on=0 skips CALL GROW (hydrology-only configs, as the LCLIM
 !     path does at HYBRID9.f90:475).
 !
+! cell_order /= 0 instead runs the reference's own order and semantics:
+! decade -> cell (y, x) -> year (HYBRID9.f90:93-130, decades 1901-1910,
+! 1911-1920, ...), with the module array smp NOT reset between cells, so
+! every cell's first substep of a decade computes beta (HYDROLOGY.f90:
+! 270-275) from the smp its predecessor in cell order left behind
+! (SHARED.f90:198).  The first land cell takes the smp the last land cell
+! holds at the start (so from the second decade on, what it left behind;
+! at a fresh start every smp is 0 -- the reference leaves smp
+! uninitialised, INIT.f90:109).  The per-cell smp written to state_end is
+! the smp each cell left behind at the end of its last decade.
+!
 ! lclim_mode /= 0 restates instead the LCLIM single-site path of
 ! HYBRID9.f90:339-480: sub-daily forcing (tak, rh, Rnet, PAR, ppt per
 ! substep, :428-439), daily huss and ps (:377-378), the day-of-year LAI
@@ -43,6 +54,7 @@ USE SHARED
 IMPLICIT NONE
 
 INTEGER :: ncell, year0, nyears, grow_on, state_override, ntrace, lclim_mode
+INTEGER :: cell_order, dsyr, deyr
 REAL, ALLOCATABLE :: lsub (:,:,:), lday (:,:,:), llai (:,:,:), out_day (:,:,:)
 INTEGER :: trace_cells (64)
 INTEGER :: ndays, iyr, itr, L, u, ios
@@ -58,13 +70,14 @@ REAL :: ps_sum, pr_sum, rhs_sum, h2osoi_sum_total
 INTEGER :: nfield
 
 NAMELIST /h9case/ ncell, NISURF, year0, nyears, grow_on, &
-                  state_override, ntrace, trace_cells, lclim_mode
+                  state_override, ntrace, trace_cells, lclim_mode, cell_order
 
 CALL GET_COMMAND_ARGUMENT (1, dir)
 IF (LEN_TRIM (dir) == 0) STOP 'usage: h9ref <casedir>'
 
 ncell = 0; NISURF = 48; year0 = 1901; nyears = 1; grow_on = 1
 state_override = 0; ntrace = 0; trace_cells = 0; lclim_mode = 0
+cell_order = 0
 OPEN (NEWUNIT=u, FILE=TRIM(dir)//'/case.nml', STATUS='OLD')
 READ (u, NML=h9case)
 CLOSE (u)
@@ -315,15 +328,27 @@ CLOSE (u)
 ELSE
 
 !----------------------------------------------------------------------!
-! Hot loops, restating HYBRID9.f90:120-290 (PGF path).
+! Hot loops, restating HYBRID9.f90:120-290 (PGF path).  Isolated-cell
+! semantics run every year of a cell at once; cell_order runs the
+! reference's decade loop (HYBRID9.f90:93-130) around the cell loop.
 !----------------------------------------------------------------------!
+DO x = 1, lon_c                               ! cell_order: chain start,
+  IF (SUM (theta_s (:,x,1)) > trunc) smp (:) = fz ((x-1)*L+1 : x*L)   ! last land cell
+END DO
+dsyr = syr
+DO WHILE (dsyr <= eyr)
+IF (cell_order /= 0) THEN
+  deyr = MIN (1901 + 10 * ((dsyr - 1901) / 10) + 9, eyr)
+ELSE
+  deyr = eyr
+END IF
 DO y = 1, lat_c
   DO x = 1, lon_c
     IF (SUM (theta_s (:,x,y)) > trunc) THEN
       do_trace = ANY (trace_cells (1:MAX(ntrace,1)) == x) .AND. ntrace > 0
-      smp (:) = fz ((x-1)*L+1 : x*L)          ! isolated-cell semantics
+      IF (cell_order == 0) smp (:) = fz ((x-1)*L+1 : x*L)   ! isolated-cell semantics
       nlayers = nsoil_layers_max
-      DO jyear = syr, eyr
+      DO jyear = dsyr, deyr
         npp_sum        = zero
         plant_mass_sum = zero
         rnf_sum  = zero
@@ -409,6 +434,8 @@ DO y = 1, lat_c
     END IF
   END DO
 END DO
+dsyr = deyr + 1
+END DO   ! decades
 
 IF (ntrace > 0) CLOSE (itr)
 

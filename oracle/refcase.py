@@ -76,7 +76,12 @@ def unpack_state(buf: np.ndarray, ncell: int, L: int) -> dict:
 
 
 def write_case(d, *, zi, params, forcing=None, nisurf=48, year0=1901, nyears=1,
-               grow_on=1, state0=None, trace_cells=(), site=None):
+               grow_on=1, state0=None, trace_cells=(), site=None, cell_order=False):
+    """cell_order: the reference's decade -> cell -> year order with smp
+    carried from cell to cell (h9ref_main.f90 cell_order) instead of
+    isolated-cell semantics."""
+    if cell_order and trace_cells:
+        raise ValueError("traces are per cell; cell_order interleaves them")
     d = Path(d)
     d.mkdir(parents=True, exist_ok=True)
     ncell = params["fmax"].size
@@ -88,7 +93,7 @@ def write_case(d, *, zi, params, forcing=None, nisurf=48, year0=1901, nyears=1,
            f" ncell={ncell}, NISURF={nisurf}, year0={year0}, nyears={nyears},\n"
            f" grow_on={int(grow_on)}, state_override={int(state0 is not None)},\n"
            f" ntrace={len(trace_cells)}, trace_cells={','.join(str(c + 1) for c in tc)},\n"
-           f" lclim_mode={int(site is not None)}\n/\n")
+           f" lclim_mode={int(site is not None)}, cell_order={int(bool(cell_order))}\n/\n")
     (d / "case.nml").write_text(nml)
     np.asarray(zi, dtype=np.float32).tofile(d / "zi.f32")
     np.concatenate([params[k].ravel() for k in ("theta_s", "hksat", "bsw", "psi_s")]

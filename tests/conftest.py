@@ -38,7 +38,7 @@ def load_golden(name):
     meta = json.loads(str(z["meta"]))
     L = meta["L"]
     n = meta["ncell"]
-    if meta["kind"] in ("synth", "bench_stop"):
+    if meta["kind"] in ("synth", "bench_stop", "cell_order"):
         gid = np.asarray(meta["gid"], dtype=np.int64)
         p, f = synth_inputs(gid, meta["year0"], meta["nyears"], L, meta["seed"])
         assert digest(packed_params(p), f) == meta["input_sha256"], "synthetic inputs drifted"

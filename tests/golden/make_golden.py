@@ -334,6 +334,78 @@ def bench_stop_case(name="c2_bench_stop", year0=1901, nyears=10, nisurf=48):
     print(f"{name}: {n} cells x {nyears} yr, STOPs {stops}")
 
 
+def rel_bound(a, b):
+    """max |a - b| / |b| over finite b != 0, and the cells where a and b
+    differ in any bit (NaN == NaN)."""
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    ok = np.isfinite(b) & (b != 0)
+    r = np.abs(a[ok] - b[ok]) / np.abs(b[ok])
+    return float(r.max()) if r.size else 0.0
+
+
+def cell_order_case(name, gid, *, year0=1901, nyears=30, nisurf=48, grow_on=1, split=None):
+    """The reference as it really runs: h9ref's cell_order
+    mode, decade -> cell -> year with smp carried from cell to cell
+    (HYBRID9.f90:93-130, HYDROLOGY.f90:270-275, SHARED.f90:198), cells in
+    the reference's (y, x) order.  Also records, as data, how far the
+    isolated-cell contract (every cell its own smp) sits from it, and
+    (split) how far the reference itself moves when its cells are cut into
+    two ranks (two chains, INIT.f90:271-274)."""
+    gid = np.asarray(gid, dtype=np.int64)
+    p, f = synth_inputs(gid, year0, nyears)
+    kw = dict(zi=synth.ZI_L8, params=p, forcing=f, nisurf=nisurf, year0=year0, nyears=nyears,
+              grow_on=grow_on)
+    co = refcase.run_case(cell_order=True, **kw)
+    iso = refcase.run_case(**kw)
+    ai, ac = iso["annual"], co["annual"]
+    L = 8
+    fields = refcase.annual_fields(L)
+    pick = [fields.index(k) for k in ["rnf", "theta_total"] + [f"theta{i + 1}" for i in range(L)]]
+    diff_cells = np.any(np.any(ai.view(np.uint32) != ac.view(np.uint32), axis=0), axis=0)
+    first_year = [int(year0 + np.argmax(np.any(ai[:, :, c].view(np.uint32) != ac[:, :, c].view(np.uint32), axis=1)))
+                  for c in np.where(diff_cells)[0]]
+    iso_bound = dict(
+        annual=rel_bound(ai[:, pick, :], ac[:, pick, :]),
+        **{k: rel_bound(iso["state"][k], co["state"][k]) for k in ("h2osoi_liq", "zwt", "wa")},
+        cells_differing=int(diff_cells.sum()),
+        first_decade_bitwise=bool(np.array_equal(ai[:min(nyears, 10)].view(np.uint32),
+                                                 ac[:min(nyears, 10)].view(np.uint32))),
+        first_year_hist={str(y): first_year.count(y) for y in sorted(set(first_year))})
+    split_bound = None
+    if split:
+        half = gid.size // 2
+        parts = []
+        for sl in (slice(0, half), slice(half, gid.size)):
+            parts.append(refcase.run_case(cell_order=True, zi=synth.ZI_L8,
+                                          params={k: v[sl] for k, v in p.items()},
+                                          forcing=np.ascontiguousarray(f[:, :, sl]), nisurf=nisurf, year0=year0,
+                                          nyears=nyears, grow_on=grow_on)["annual"])
+        a2 = np.concatenate(parts, axis=2)
+        split_bound = dict(annual=rel_bound(a2[:, pick, :], ac[:, pick, :]),
+                           cells_differing=int(np.any(np.any(a2.view(np.uint32) != ac.view(np.uint32), axis=0),
+                                                      axis=0).sum()))
+    meta = dict(name=name, kind="cell_order", seed=synth.SEED, gid=gid.tolist(), L=L, ncell=int(gid.size),
+                year0=year0, nyears=nyears, nisurf=nisurf, grow_on=grow_on, zi=synth.ZI_L8.tolist(),
+                input_sha256=digest(packed_params(p), f), isolated_vs_cell_order=iso_bound,
+                two_ranks_vs_one=split_bound,
+                generator="oracle/_ref/h9ref cell_order=1 (reference HYDROLOGY.f90/GROW.f90, amdflang -O2; "
+                          "decade -> cell -> year, smp carried between cells)")
+    np.savez_compressed(OUT / f"{name}.npz", meta=np.array(json.dumps(meta)), annual=ac,
+                        state=refcase.pack_state(co["state"], L))
+    print(f"{name}: {gid.size} cells x {nyears} yr, isolated vs cell order {iso_bound}, two ranks {split_bound}, "
+          f"{(OUT / f'{name}.npz').stat().st_size / 1e3:.0f} kB")
+
+
+def main_cell_order():
+    g10 = np.array([(80 + j) * synth.NX05 + 400 + i for j in range(10) for i in range(10)])
+    # config 1's grid over three decades (1901-1930)
+    cell_order_case("co_c1_30yr", g10, nyears=30, split=True)
+    # a contiguous 0.5 deg row band (rows 150-157: 2,022 land cells) over two decades
+    land = synth.land_cells()
+    rows = land // synth.NX05
+    cell_order_case("co_band", land[(rows >= 150) & (rows < 158)], nyears=20)
+
+
 def site_inputs(gid, L, nisurf, years, events, seed=synth.SEED, soils="synth", ppt_scale=1.0):
     """Synthetic LCLIM site inputs (hybrid9_amd.site): soils of the land
     cells gid (soils="independent": independent_layer_params), site forcing
@@ -418,6 +490,7 @@ def main():
     spinup_case()
     l10_case()
     bench_stop_case()
+    main_cell_order()
 
 
 if __name__ == "__main__":
