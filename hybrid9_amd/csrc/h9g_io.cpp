@@ -868,6 +868,7 @@ int h9g_nc_read_groups(const char *const *paths, int nx, int ny, int ncell, cons
         cl.cells[(size_t)(y / cl.cy) * cl.nbx + (size_t)(x / cl.cx)].push_back(
             {c, (uint32_t)((y % cl.cy) * cl.cx + x % cl.cx)});
       }
+      const size_t j0 = jobs.size();
       for (size_t i = 0; i < s.ck.ch.size(); i++) {
         const auto &ch = s.ck.ch[i];
         if (ch.c[0] + s.ck.cd[0] <= (hsize_t_)t0 || ch.c[0] >= (hsize_t_)(t0 + nt)) continue;
@@ -876,6 +877,20 @@ int h9g_nc_read_groups(const char *const *paths, int nx, int ny, int ncell, cons
           const int d1 = (int)std::min<hsize_t_>(ch.c[0] + s.ck.cd[0], (hsize_t_)(t0 + nt)) - t0;
           jobs.push_back({k, i, d0, d1});
         }
+      }
+      // The chunk table lists only the chunks that were written.  A chunk
+      // holding cells of the days asked for that was never written (its
+      // values are the fill value) has no entry: then the file is read
+      // through H5Dread, which fills it, as the reference's nf90_get_var
+      // does.  Entries are unique by their coordinates, so
+      // the count decides.
+      size_t cols_used = 0;
+      for (const auto &v : cl.cells) cols_used += !v.empty();
+      const size_t tchunks = (size_t)((hsize_t_)(t0 + nt - 1) / s.ck.cd[0] - (hsize_t_)t0 / s.ck.cd[0] + 1);
+      if (jobs.size() - j0 != tchunks * cols_used) {
+        jobs.resize(j0);
+        s.kind = 2;
+        jobs.push_back({k, 0, 0, nt});
       }
     } else if (s.kind == 3) {
       for (int t = 0; t < nt; t++) jobs.push_back({k, (size_t)t, t, t + 1});
@@ -896,6 +911,10 @@ int h9g_nc_read_groups(const char *const *paths, int nx, int ny, int ncell, cons
   for (auto &p : pending) p = 0;
   for (const Job &jb : jobs)
     for (int g = group_of(jb.d0); g <= group_of(jb.d1 - 1); g++) pending[(size_t)g]++;
+  // a group no job fills (cannot happen with every file covering every
+  // day; kept so that a prefetch never waits on a copy nobody queues)
+  for (int g = 0; g < ngroups; g++)
+    if (pending[(size_t)g] == 0 && done) done(gd(g), gd(g + 1));
   const int nw = io_threads();
   struct Scratch {
     std::vector<unsigned char> raw, tmp;

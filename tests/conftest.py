@@ -13,9 +13,32 @@ GOLDEN = ROOT / "tests" / "golden"
 sys.path.insert(0, str(ROOT))
 
 
+_CRASH_LOG = None
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long CPU test")
+    # A fatal error (segfault, abort) in native code kills the interpreter
+    # before pytest reports which test ran (one CPU run of six
+    # died that way).  Every test's id is written, flushed, to
+    # tests/_build/crash.log before it runs, and faulthandler dumps every
+    # thread's Python stack into the same file, so the last id in it names
+    # the test a crash happened in.
+    global _CRASH_LOG
+    import faulthandler
+    d = ROOT / "tests" / "_build"
+    d.mkdir(parents=True, exist_ok=True)
+    _CRASH_LOG = open(d / "crash.log", "w", buffering=1)
+    faulthandler.enable(file=_CRASH_LOG, all_threads=True)
+
+
+def pytest_runtest_logstart(nodeid, location):
+    if _CRASH_LOG is not None:
+        import os
+        _CRASH_LOG.write(f"== {nodeid}\n")
+        _CRASH_LOG.flush()
+        os.fsync(_CRASH_LOG.fileno())
 
 
 def golden_names(kind=None):

@@ -94,19 +94,26 @@ def nc4_writer_bin() -> Path | None:
                              f"-L{CONDA}/lib", f"-Wl,-rpath,{CONDA}/lib", "-lhdf5_hl", "-lhdf5"])
 
 
-def write_nc4(path: Path, var: str, data: np.ndarray, chunk=None, filters: str | None = None) -> Path:
+NC_FILL_FLOAT = np.float32(9.9692099683868690e+36)   # netCDF's default float fill (nc4_write.c)
+
+
+def write_nc4(path: Path, var: str, data: np.ndarray, chunk=None, filters: str | None = None,
+              skip: int | None = None) -> Path:
     """A netCDF-4 (HDF5) file with <var>(time, lat, lon) and its coordinate
     dimension scales (nc4_write.c); chunk (ct, cy, cx) and filters
     ("s" shuffle, "d" deflate, "f" fletcher32, "b" big-endian) default to one
-    chunk per day, shuffle + deflate."""
+    chunk per day, shuffle + deflate.  skip: a day whose time chunks are
+    never written (they read as NC_FILL_FLOAT)."""
     exe = nc4_writer_bin()
     raw = path.with_suffix(".raw")
     np.ascontiguousarray(data, np.float32).tofile(raw)
     nt, ny, nx = data.shape
     extra = []
-    if chunk is not None or filters is not None:
+    if chunk is not None or filters is not None or skip is not None:
         ct, cy, cx = chunk if chunk is not None else (1, ny, nx)
-        extra = [str(ct), str(cy), str(cx)] + ([filters] if filters is not None else [])
+        extra = [str(ct), str(cy), str(cx)] + ([filters if filters is not None else "sd"]
+                                               if filters is not None or skip is not None else [])
+        extra += [str(skip)] if skip is not None else []
     subprocess.run([str(exe), str(path), var, str(nt), str(ny), str(nx), str(raw), *extra], check=True)
     raw.unlink()
     return path

@@ -196,6 +196,31 @@ def test_forcing_reader_netcdf4_chunk_layouts(tmp_path, chunk, filters, monkeypa
 
 
 @pytest.mark.skipif(not Path("/opt/conda/include/hdf5.h").exists(), reason="no HDF5 in this image")
+@pytest.mark.parametrize("chunk", [(1, NY, NX), (4, 5, 7)])
+def test_forcing_reader_netcdf4_unwritten_chunk(tmp_path, chunk, monkeypatch):
+    """A time chunk that was never written has no entry in the chunk table
+    (ADVICE r04): the reader must return the fill value there, as H5Dread /
+    nf90_get_var do, not what the output buffer held before.  The file of
+    one variable misses the chunks of day 6; the days read span it."""
+    from tests.helpers import NC_FILL_FLOAT, write_nc4
+    rng = np.random.default_rng(12)
+    nt = 17
+    data = [rng.uniform(200, 300, (nt, NY, NX)).astype(np.float32) for _ in range(7)]
+    paths = [write_nc4(tmp_path / f"{v}_pgfv2.1_1901-1910.nc4", v, data[k], chunk, "sd", skip=6 if k == 3 else None)
+             for k, v in enumerate(h.PGF_VARS)]
+    gid = np.sort(rng.choice(NX * NY, 29, replace=False)).astype(np.int64)
+    exp = np.stack([data[k].reshape(nt, -1)[2:15][:, gid] for k in range(7)])
+    ct = chunk[0]
+    for t in range(2, 15):
+        if t // ct == 6 // ct:
+            exp[3, t - 2] = NC_FILL_FLOAT
+    for threads in ("1", "5"):
+        monkeypatch.setenv("H9G_IO_THREADS", threads)
+        got = h.nc_forcing_read(paths, NX, NY, gid, 2, 13)
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), threads
+
+
+@pytest.mark.skipif(not Path("/opt/conda/include/hdf5.h").exists(), reason="no HDF5 in this image")
 def test_synthetic_pgf_files_round_trip(tmp_path):
     """tools/pgf_synth.py (the files bench.py --forcing nc4 reads each step)
     holds the bench's own synthetic forcing at the land cells: read back
