@@ -128,6 +128,7 @@ def lib() -> C.CDLL:
         "h9g_nc_forcing_read": (C.c_int, [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_int, _I64P,
                                           C.c_int, C.c_int, _FP]),
         "h9g_nc_ntimes": (C.c_int, [C.c_char_p]),
+        "h9g_nc_read_stats": (C.c_int, [C.POINTER(C.c_double), C.c_int]),
         "h9g_nc_forcing_prefetch": (C.c_int, [vp, C.c_int, C.POINTER(C.c_char_p), C.c_int, C.c_int,
                                               C.c_int, C.c_int]),
         "h9g_soil_layer": (C.c_int, [vp, C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_int]),
@@ -446,6 +447,18 @@ def pgf_paths(directory, decade: str, suffix: str = "nc4"):
 def nc_ntimes(path) -> int:
     """NTIMES of a PGF file (its 'time' dimension, READ_NET_CDF_0D.f90)."""
     return _check(lib().h9g_nc_ntimes(str(path).encode()), "h9g_nc_ntimes")
+
+
+IO_STATS = ("wall_s", "setup_s", "threads", "jobs", "pread_s", "inflate_s", "gather_s", "other_s",
+            "bytes_read", "bytes_decoded", "values", "pool_wall_s")
+
+
+def nc_read_stats() -> dict:
+    """Stage profile of the last forcing read (h9g_nc_read_stats): wall and
+    setup seconds, then thread-seconds per stage summed over the pool."""
+    out = (C.c_double * len(IO_STATS))()
+    m = _check(lib().h9g_nc_read_stats(out, len(IO_STATS)), "h9g_nc_read_stats")
+    return {k: float(out[i]) for i, k in enumerate(IO_STATS[:m])}
 
 
 def nc_forcing_read(paths, nx: int, ny: int, gid, t0: int, nt: int) -> np.ndarray:

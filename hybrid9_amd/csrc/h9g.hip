@@ -127,6 +127,10 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   __shared__ double s_l2[32];
   __shared__ float s_cell[H9G_PWAVES][PS::ROWS * H9G_PLANES];   // [wave][row][lane]
   __shared__ float s_zt[zt_size<L>()];
+  // the day snapshot addresses its global block by LDS byte offset
+  // (PairStore::svw): every static LDS address must lie inside GBLOCK
+  static_assert(sizeof(s_e2) + sizeof(s_l2) + sizeof(s_cell) + sizeof(s_zt) <= (size_t)PS::GBLOCK,
+                "pair kernel LDS footprint exceeds the day-snapshot block");
   if (threadIdx.x == 0) fill_zt<L>(g, s_zt);
   load_tabs(s_e2, s_l2);
   const h9m::Tabs T = {s_e2, s_l2};
@@ -1532,7 +1536,7 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
   }
   if (kind != 2) {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
-    const size_t need = ((ctx->n + per_block - 1) / per_block) * 65536;
+    const size_t need = ((ctx->n + per_block - 1) / per_block) * PairStore<8, H9G_PLANES>::GBLOCK;
     if (ctx->sv_bytes < need) {
       (void)hipFree(ctx->d_sv);
       ctx->d_sv = nullptr;

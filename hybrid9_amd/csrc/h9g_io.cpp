@@ -59,6 +59,18 @@ int type_size(int t) {
 }
 size_t pad4(size_t n) { return (n + 3) & ~(size_t)3; }
 
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+// Stage times of the last forcing read (h9g_nc_read_stats): thread-seconds
+// summed over the pool, so that a stage's share of the pool is its sum over
+// (wall x threads).
+std::mutex g_stats_lock;
+double g_stats[H9G_IO_NSTATS];
+
 // ------------------------------------------------------------------ reader
 struct NcVar {
   std::string name;
@@ -519,10 +531,17 @@ struct Chunked {               // a (time, lat, lon) field stored as filtered ch
     }
   };
   bool decode(int fd, const Ch &c, std::vector<unsigned char> &raw, std::vector<unsigned char> &tmp, View &out,
-              void *&zst) const {
+              void *&zst, double *t_stage) const {
     const size_t nb = chunk_bytes();
     raw.resize((size_t)c.size);
+    const double ta = now_s();
     if (pread(fd, raw.data(), (size_t)c.size, (off_t)c.addr) != (ssize_t)c.size) return false;
+    const double tb = now_s();
+    t_stage[0] += tb - ta;
+    struct Tail {                                 // the rest is inflate / unshuffle time
+      double t0, *acc;
+      ~Tail() { *acc += now_s() - t0; }
+    } tail{tb, t_stage + 1};
     std::vector<unsigned char> *cur = &raw, *spare = &tmp;
     bool planes = false;
     for (int i = nfilt - 1; i >= 0; i--) {        // undo the pipeline in reverse
@@ -791,6 +810,7 @@ int h9g_nc_forcing_read(const char *const *paths, int nx, int ny, int ncell, con
 int h9g_nc_read_groups(const char *const *paths, int nx, int ny, int ncell, const int64_t *gid, int t0, int nt,
                        float *out, int ngroups, const std::function<void(int, int)> &done) {
   if (!paths || nx <= 0 || ny <= 0 || ncell <= 0 || !gid || t0 < 0 || nt < 1 || !out) return H9G_EINVAL;
+  const double tstart = now_s();
   ngroups = std::max(1, std::min(ngroups, nt));
   int64_t ymin = ny, ymax = -1;
   for (int c = 0; c < ncell; c++) {
@@ -920,6 +940,8 @@ int h9g_nc_read_groups(const char *const *paths, int nx, int ny, int ncell, cons
     std::vector<unsigned char> raw, tmp;
     std::vector<float> vals;
     void *z = nullptr;
+    double t[4] = {0, 0, 0, 0};          // pread, inflate + unshuffle, gather, other layouts (s)
+    double bytes_in = 0, bytes_out = 0, values = 0, jobs = 0;
   };
   std::vector<Scratch> scr((size_t)nw);
   std::mutex h5lock;                                // kind 2 goes through HDF5
@@ -932,7 +954,8 @@ int h9g_nc_read_groups(const char *const *paths, int nx, int ny, int ncell, cons
     if (s.kind == 1) {
       const auto &ch = s.ck.ch[jb.i];
       Chunked::View v;
-      if (!s.ck.decode(s.fd, ch, sc.raw, sc.tmp, v, sc.z)) return false;
+      if (!s.ck.decode(s.fd, ch, sc.raw, sc.tmp, v, sc.z, sc.t)) return false;
+      const double tg = now_s();
       const Cols &cl = cols[(size_t)jb.k];
       const auto &cells = cl.cells[(size_t)(ch.c[1] / cl.cy) * cl.nbx + (size_t)(ch.c[2] / cl.cx)];
       const size_t cplane = (size_t)(cl.cy * cl.cx);
@@ -943,8 +966,17 @@ int h9g_nc_read_groups(const char *const *paths, int nx, int ny, int ncell, cons
         float *o = out + ((size_t)jb.k * nt + (size_t)(t - (hsize_t_)t0)) * ncell;
         for (const auto &p : cells) o[p.first] = v.value(e0 + p.second);
       }
+      sc.t[2] += now_s() - tg;
+      sc.bytes_in += (double)ch.size;
+      sc.bytes_out += (double)s.ck.chunk_bytes();
+      sc.values += (double)cells.size() * (double)(tb - ta);
       return true;
     }
+    const double to = now_s();
+    struct Tail {
+      double t0, *acc;
+      ~Tail() { *acc += now_s() - t0; }
+    } tail{to, sc.t + 3};
     if (s.kind == 3) {                              // classic: rows [ymin, ymax] of day t0 + i
       const NcReader &r = s.nc;
       const NcVar &v = *s.v;
@@ -973,17 +1005,43 @@ int h9g_nc_read_groups(const char *const *paths, int nx, int ny, int ncell, cons
     }
     return true;
   };
+  const double tpool = now_s();
   const bool ok = run_pool(jobs.size(), [&](size_t j, int w) -> bool {
-    if (!one(jobs[j], scr[(size_t)w % scr.size()])) return false;
+    Scratch &sc = scr[(size_t)w % scr.size()];
+    if (!one(jobs[j], sc)) return false;
+    sc.jobs += 1;
     finish(jobs[j]);
     return true;
   });
+  const double tend = now_s();
   for (auto &sc : scr)
     if (sc.z && inflater().release) inflater().release(sc.z);
+  {
+    std::lock_guard<std::mutex> g(g_stats_lock);
+    double st[H9G_IO_NSTATS] = {tend - tstart, tpool - tstart,
+                                (double)std::min<size_t>((size_t)nw, std::max<size_t>(jobs.size(), 1)), 0, 0, 0, 0,
+                                0, 0, 0, 0, tend - tpool};
+    for (auto &sc : scr) {
+      st[3] += sc.jobs;
+      for (int i = 0; i < 4; i++) st[4 + i] += sc.t[i];
+      st[8] += sc.bytes_in;
+      st[9] += sc.bytes_out;
+      st[10] += sc.values;
+    }
+    memcpy(g_stats, st, sizeof st);
+  }
   return ok ? 0 : H9G_EINVAL;
 }
 
 extern "C" {
+
+int h9g_nc_read_stats(double *out, int n) {
+  if (!out || n < 1) return H9G_EINVAL;
+  std::lock_guard<std::mutex> g(g_stats_lock);
+  const int m = std::min(n, (int)H9G_IO_NSTATS);
+  memcpy(out, g_stats, sizeof(double) * (size_t)m);
+  return m;
+}
 
 // NTIMES of a PGF file (READ_NET_CDF_0D.f90: the 'time' dimension).
 int h9g_nc_ntimes(const char *path) {

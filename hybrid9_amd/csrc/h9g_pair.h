@@ -1887,7 +1887,7 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
     cs.day_start(day);
     H9G_BR(BR_DAY);
 #if defined(H9G_DUMP_AQ) && defined(__HIP_DEVICE_COMPILE__)
-    if (h9g_aq_bits && s.zwt > g.zim(L)) {
+    if (act && h9g_aq_bits && s.zwt > g.zim(L)) {   // spare lanes hold a mirrored cell's stale zwt
       const size_t c = (size_t)((const float *)acc - h9g_aq_base);
       atomicOr(&h9g_aq_bits[c * 12 + day / 32], 1u << (day & 31));
     }

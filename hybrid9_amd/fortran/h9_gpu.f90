@@ -235,6 +235,12 @@ INTERFACE
     CHARACTER(KIND=C_CHAR), INTENT(IN) :: path (*)
     INTEGER(C_INT) :: h9g_nc_ntimes
   END FUNCTION
+  FUNCTION h9g_nc_read_stats (out, n) BIND(C, NAME='h9g_nc_read_stats')
+    IMPORT :: C_INT, C_DOUBLE
+    REAL(C_DOUBLE), INTENT(OUT) :: out (*)
+    INTEGER(C_INT), VALUE :: n
+    INTEGER(C_INT) :: h9g_nc_read_stats
+  END FUNCTION
   FUNCTION h9g_nc_forcing_prefetch (ctx, slot, paths, nx, ny, t0, nt) &
       BIND(C, NAME='h9g_nc_forcing_prefetch')
     IMPORT :: C_INT, C_PTR

@@ -225,6 +225,14 @@ int h9g_nc_forcing_read(const char *const *paths, int nx, int ny, int ncell,
                         const int64_t *gid, int t0, int nt, float *out);
 /* NTIMES of a PGF file: length of its 'time' dimension. */
 int h9g_nc_ntimes(const char *path);
+/* Stage profile of the last completed forcing read (any thread, any
+ * context): out[0..n) of, in order, wall s, serial setup s (headers and
+ * chunk tables), pool threads, jobs, then thread-seconds summed over the
+ * pool of pread, inflate + unshuffle, gather, and other layouts (classic
+ * rows / H5Dread), then stored bytes read, bytes decoded, values gathered
+ * and the pool's wall s.  Returns the count written (<= H9G_IO_NSTATS). */
+#define H9G_IO_NSTATS 12
+int h9g_nc_read_stats(double *out, int n);
 /* The same read on a host thread into pinned memory, then an async copy
  * into `slot` (needs h9g_set_cells); h9g_run_year on the slot waits. */
 int h9g_nc_forcing_prefetch(h9g_ctx *ctx, int slot, const char *const *paths,

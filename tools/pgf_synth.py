@@ -59,13 +59,31 @@ def write_year(directory, year: int = 1901, ndays: int = 366, seed: int = synth.
 
 
 def time_read(paths, ndays: int, gid, nx: int = synth.NX05, ny: int = synth.NY05, reps: int = 2) -> dict:
-    ts = []
+    ts, stats = [], []
     out = None
     for _ in range(reps):
         t = time.perf_counter()
         out = h.nc_forcing_read(paths, nx, ny, gid, 0, ndays)
         ts.append(time.perf_counter() - t)
-    return dict(seconds=min(ts), all=ts, out=out)
+        stats.append(h.nc_read_stats())
+    best = int(np.argmin(ts))
+    return dict(seconds=ts[best], all=ts, out=out, stats=stats[best])
+
+
+def stage_report(s: dict) -> str:
+    """One line per stage of h9g_nc_read_stats: thread-seconds, share of
+    the pool (wall x threads) and per-thread rate."""
+    pool = s["pool_wall_s"] * s["threads"]
+    busy = s["pread_s"] + s["inflate_s"] + s["gather_s"] + s["other_s"]
+    lines = [f"  wall {s['wall_s']:.3f} s = setup {s['setup_s']:.3f} s + pool {s['pool_wall_s']:.3f} s "
+             f"x {s['threads']:.0f} threads, {s['jobs']:.0f} jobs; busy {busy / max(pool, 1e-12):.2f} of the pool"]
+    for k, what, b in (("pread_s", "stored bytes", s["bytes_read"]), ("inflate_s", "decoded bytes", s["bytes_decoded"]),
+                       ("gather_s", "values", s["values"]), ("other_s", "", 0)):
+        if s[k] <= 0:
+            continue
+        rate = f", {b / s[k] / 1e9:.2f} G{what} per thread-s" if b else ""
+        lines.append(f"  {k[:-2]:8s} {s[k]:7.3f} thread-s ({s[k] / max(pool, 1e-12):.2f} of the pool){rate}")
+    return "\n".join(lines)
 
 
 def main() -> None:
@@ -96,6 +114,7 @@ def main() -> None:
     print(f"h9g_nc_forcing_read: {a.days} days x {gs.size} cells (shard {a.shard}): "
           f"{r['seconds']:.3f} s (runs {', '.join(f'{x:.3f}' for x in r['all'])}), "
           f"{a.days * 365.0 / a.days:.0f}-day year: {r['seconds'] * 365.0 / a.days:.3f} s")
+    print(stage_report(r["stats"]))
     if a.check:
         ref = synth.make_forcing(gs, synth.cell_lat(gs), synth.year_day0(a.year), a.days)
         ok = np.array_equal(ref.view(np.uint32), r["out"].view(np.uint32))
