@@ -399,10 +399,37 @@ def diag_exchange(ctx, torch, dist, device: str):
     return exchange, buf
 
 
-def timed_steps(ctx, pl: dict, exchange, sync) -> float:
+def ordered_years(ctx, pl: dict, s0: int, s1: int, exchange, work: list) -> None:
+    """Steps s0 .. s1-1 in the reference's own cell order: the reference's
+    decades (HYBRID9.f90:93-130) cut to the range, one
+    h9g_run_decade_ordered each (smp carried from cell to cell)."""
+    import hybrid9_amd as h
+    if s1 <= s0:
+        return
+    for y0, ny in h.decades(pl["years"][s0], s1 - s0):
+        s = pl["years"].index(y0)
+        ctx.run_decade_ordered([pl["slot_of_step"][k] for k in range(s, s + ny)], y0, raise_on_stop=False,
+                               annual=False)
+        work.append(dict(ctx.decade_stats(), years=ny))
+        if exchange:
+            exchange()
+
+
+def timed_steps(ctx, pl: dict, exchange, sync, order: str = "isolated", work: list | None = None) -> float:
     """W untimed warmup years, then K timed years between two `sync`s
-    (barrier + device synchronisation).  Returns the elapsed seconds."""
+    (barrier + device synchronisation).  Returns the elapsed seconds.
+    order "cell": the years in the reference's cell order (ordered_years;
+    `work` collects each decade's h9g_decade_stats)."""
     W, K = pl["W"], pl["K"]
+    if order == "cell":
+        work = [] if work is None else work
+        ordered_years(ctx, pl, 0, W, exchange, [])
+        sync()
+        ctx.total_kernel_ms(reset=True)
+        t0 = time.perf_counter()
+        ordered_years(ctx, pl, W, W + K, exchange, work)
+        sync()
+        return time.perf_counter() - t0
     for s in range(W):
         ctx.run_year(pl["slot_of_step"][s], pl["years"][s])
         if exchange:
@@ -432,12 +459,18 @@ def main():
     ap.add_argument("--host-fed", action="store_true",
                     help="PCIe-inclusive rate: every step's forcing year is copied from pinned host "
                          "memory (async, double-buffered); reported in DESIGN.md, never as `value`")
+    ap.add_argument("--order", choices=["isolated", "cell"], default="isolated",
+                    help="cell: the reference's own cell order (h9g_run_decade_ordered per decade, smp "
+                         "carried from cell to cell, bit-identical to the reference); isolated: every cell "
+                         "its own smp (h9g_run_year per year)")
     ap.add_argument("--forcing", choices=["device", "nc4"], default="device",
                     help="nc4: every step's forcing is read from synthetic PGF netCDF-4 files through "
                          "h9g_nc_forcing_prefetch (ingest-inclusive; DESIGN.md, never as `value`)")
     args = ap.parse_args()
     if args.forcing == "nc4" and (args.host_fed or WORKLOADS[args.workload]["grid"] != "05"):
         raise SystemExit("--forcing nc4: 0.5 deg workloads only, not with --host-fed")
+    if args.order == "cell" and (args.host_fed or args.forcing != "device"):
+        raise SystemExit("--order cell: resident device forcing only")
     wl = WORKLOADS[args.workload]
     K = args.steps if args.steps is not None else wl.get("steps", 3)
     W = args.warmup if args.warmup is not None else wl.get("warmup", 1)
@@ -503,7 +536,8 @@ def main():
         barrier_sync(ctx, torch, dist, world)
 
     runner = _Fed(ctx) if host_fed else (_NcFed(ctx) if nc_fed else ctx)
-    elapsed = timed_steps(runner, pl, exchange, sync)
+    work = []
+    elapsed = timed_steps(runner, pl, exchange, sync, args.order, work)
     kern_ms = ctx.total_kernel_ms(reset=True)
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
@@ -562,7 +596,12 @@ def main():
         "cpu_baseline": None,
         "diagnostics_last_year": {k: float(v) for k, v in zip(h.DIAG_NAMES, diag)},
         "cells_stopped": failed,
+        "order": args.order,
     }
+    if args.order == "cell":
+        out["cell_order"] = {"decades": work,
+                             "rerun_cell_years_per_cell_year": sum(w["rerun_cell_years"] for w in work) /
+                             max(1.0, float(gid.size * K))}
     if host_fed is not None:
         out["host_fed"] = host_fed.describe()
         host_fed.close()

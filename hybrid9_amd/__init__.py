@@ -104,6 +104,7 @@ def lib() -> C.CDLL:
         "h9g_run_year": (C.c_int, [vp, C.c_int, C.c_int]),
         "h9g_run_decade_ordered": (C.c_int, [vp, C.POINTER(C.c_int32), C.c_int, C.c_int, _FP,
                                              C.POINTER(C.c_int32)]),
+        "h9g_decade_stats": (C.c_int, [vp, C.POINTER(C.c_int64), C.c_int]),
         "h9g_sync": (C.c_int, [vp]),
         "h9g_last_error": (C.c_int, [vp, C.POINTER(_Error)]),
         "h9g_get_errors": (C.c_int, [vp, C.POINTER(C.c_int32)]),
@@ -342,20 +343,28 @@ class Context:
     def run_year(self, slot: int, jyear: int):
         _check(self._lib.h9g_run_year(self._h, slot, jyear), "h9g_run_year")
 
-    def run_decade_ordered(self, slots, jyear0: int, raise_on_stop: bool = True):
+    def run_decade_ordered(self, slots, jyear0: int, raise_on_stop: bool = True, annual: bool = True):
         """One decade of the reference's own cell order (h9g_run_decade_ordered:
         smp carried from cell to cell, HYBRID9.f90:93-130); synchronous.
-        Returns (annual (nyears, 12+L, ncell), passes); self.decade_rc holds
-        the STOP code."""
+        Returns (annual (nyears, 12+L, ncell) or None, passes);
+        self.decade_rc holds the STOP code."""
         sl = np.ascontiguousarray(slots, dtype=np.int32)
-        out = np.empty((sl.size, 12 + self.L, self.ncell), dtype=np.float32)
+        out = np.empty((sl.size, 12 + self.L, self.ncell), dtype=np.float32) if annual else None
         np_ = C.c_int32(0)
         rc = _check(self._lib.h9g_run_decade_ordered(self._h, sl.ctypes.data_as(C.POINTER(C.c_int32)), jyear0,
-                                                     sl.size, _fp(out), C.byref(np_)), "h9g_run_decade_ordered")
+                                                     sl.size, _fp(out) if annual else None, C.byref(np_)),
+                    "h9g_run_decade_ordered")
         self.decade_rc = rc
         if rc and raise_on_stop:
             raise ReferenceStop(self.last_error())
         return out, int(np_.value)
+
+    def decade_stats(self) -> dict:
+        """Work of the last run_decade_ordered (h9g_decade_stats)."""
+        out = (C.c_int64 * 4)()
+        _check(self._lib.h9g_decade_stats(self._h, out, 4), "h9g_decade_stats")
+        return dict(passes=int(out[0]), rerun_cells=int(out[1]), rerun_cell_years=int(out[2]),
+                    rerun_launches=int(out[3]))
 
     def run_site(self, sub, daily, lai, raise_on_stop: bool = True) -> np.ndarray:
         """LCLIM site path (HYBRID9.f90:339-480) over nday days, synchronous.
@@ -498,7 +507,7 @@ def run_cell_order(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow
     """``run`` in the reference's own cell order: decade by decade through
     ``Context.run_decade_ordered`` (smp carried from cell to cell, cells in
     the given order).  Returns dict(annual, state, rc, err, errors, passes
-    (per decade))."""
+    (per decade), work (decade_stats per decade))."""
     L = params["theta_s"].shape[1]
     n = params["fmax"].size
     with Context(n, zi, nlayers=L, nisurf=nisurf, grow_on=grow_on, device=device, nslots=10) as ctx:
@@ -508,7 +517,7 @@ def run_cell_order(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow
         else:
             ctx.set_state(state0)
         ann = np.full((nyears, 12 + L, n), np.nan, dtype=np.float32)
-        d0, rc, err, passes = 0, 0, None, []
+        d0, rc, err, passes, work = 0, 0, None, [], []
         for y0, ny in decades(year0, nyears):
             for k in range(ny):
                 nt = days_in_year(y0 + k)
@@ -517,11 +526,13 @@ def run_cell_order(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow
             a, p = ctx.run_decade_ordered(list(range(ny)), y0, raise_on_stop=False)
             ann[y0 - year0:y0 - year0 + ny] = a
             passes.append(p)
+            work.append(ctx.decade_stats())
             rc = ctx.decade_rc
             if rc:
                 err = ctx.last_error()
                 break
-        return dict(annual=ann, state=ctx.get_state(), rc=rc, err=err, errors=ctx.get_errors(), passes=passes)
+        return dict(annual=ann, state=ctx.get_state(), rc=rc, err=err, errors=ctx.get_errors(), passes=passes,
+                    work=work)
 
 
 def run(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=True,

@@ -442,6 +442,36 @@ __global__ void __launch_bounds__(256) h9g_restart_kernel(int m, int n, int L, c
   for (int r = 0; r < 4; r++) err[(size_t)r * n + k] = err0[(size_t)r * n + k];
 }
 
+// A re-run cell's trajectory against the one its last run took (ckpt: the
+// state and STOP record at the end of the same year).  The state and the
+// STOP record are everything a year carries into the next (the c4_spinup
+// decade carry), so a cell whose end-of-year state equals the old one's bit
+// for bit runs the rest of the decade exactly as it did: it leaves the
+// re-run with the old run's end-of-decade state (ckpt_last), its later
+// annual means stand, and keep[j] = 0.  Otherwise its new state becomes the
+// checkpoint and it runs on (keep[j] = 1).
+__global__ void __launch_bounds__(256) h9g_merge_kernel(int m, int n, int rows, const int *__restrict__ list,
+                                                        float *__restrict__ st, int *__restrict__ err,
+                                                        float *__restrict__ ckpt, int *__restrict__ eckpt,
+                                                        const float *__restrict__ ckpt_last,
+                                                        const int *__restrict__ eckpt_last, int *__restrict__ keep) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const int k = list[j];
+  bool same = true;
+  for (int r = 0; r < rows; r++)
+    same &= __float_as_uint(st[(size_t)r * n + k]) == __float_as_uint(ckpt[(size_t)r * n + k]);
+  for (int r = 0; r < 4; r++) same &= err[(size_t)r * n + k] == eckpt[(size_t)r * n + k];
+  if (same) {
+    for (int r = 0; r < rows; r++) st[(size_t)r * n + k] = ckpt_last[(size_t)r * n + k];
+    for (int r = 0; r < 4; r++) err[(size_t)r * n + k] = eckpt_last[(size_t)r * n + k];
+  } else {
+    for (int r = 0; r < rows; r++) ckpt[(size_t)r * n + k] = st[(size_t)r * n + k];
+    for (int r = 0; r < 4; r++) eckpt[(size_t)r * n + k] = err[(size_t)r * n + k];
+  }
+  keep[j] = !same;
+}
+
 // Cell order of the next year kernel: a stable counting sort of the cells
 // by where their water table was over the last year, failed cells last.
 // Cells are independent, so the order changes no result; it makes the 22
@@ -922,6 +952,7 @@ struct h9g_ctx {
   float *d_forc_s = nullptr;      // the year's forcing in slot order (h9g_perm_forcing_kernel)
   float *d_ann_s = nullptr;       // the year kernel's annual sums in slot order
   unsigned *d_aqbits = nullptr;   // H9G_DUMP_AQ builds: day-level water-table record of the last year
+  int64_t dec_stats[4] = {0, 0, 0, 0};   // last h9g_run_decade_ordered (h9g_decade_stats)
   int *d_hist = nullptr;          // per cell: substeps of the last year below the column (-1: none)
   int hist_nsub = 0;              // substeps of that year
   unsigned *d_pace = nullptr;     // Pacer mode 2 progress rows (h9g_pair.h)
@@ -1651,6 +1682,16 @@ int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) { return run_year_impl(ctx, 
 // no input changes every cell has run from the input the reference gives
 // it.  The chain's first cell never changes after pass 0, so pass p fixes
 // at least chain position p: at most m passes.
+//
+// A re-run stops early.  The input smp reaches a cell's decade only through
+// beta of its first substep (HYDROLOGY.f90:270-275), and the perturbation
+// it starts is rounded away within months in most cells: from then on the
+// cell runs bit for bit as before.  Every run therefore checkpoints each
+// cell's state and STOP record at every year end (ckpt), and after each
+// re-run year h9g_merge_kernel drops the cells whose state is the
+// checkpoint's again: they keep the old trajectory's later years and end
+// state (and so the input their successor already has).  Pass 1 then costs
+// about one year for most cells instead of ten.
 int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int nyears, float *annual, int32_t *passes) {
   if (!ctx || !slots || nyears < 1 || nyears > ctx->cfg.nslots) return H9G_EINVAL;
   if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
@@ -1674,16 +1715,21 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
   }
   const int m = (int)chain.size();
   const size_t srows = (size_t)h9g_state_size(L);
-  float *d_st0 = nullptr, *d_guess = nullptr, *d_ann_dec = nullptr;
-  int *d_err0 = nullptr, *d_chain = nullptr, *d_list = nullptr, *d_flag = nullptr;
+  float *d_st0 = nullptr, *d_guess = nullptr, *d_ann_dec = nullptr, *d_ck = nullptr;
+  int *d_err0 = nullptr, *d_chain = nullptr, *d_list = nullptr, *d_flag = nullptr, *d_eck = nullptr;
   int rc = 0, np = 0;
+  int64_t rerun_cells = 0, rerun_cell_years = 0, rerun_launches = 0;
+  auto ck = [&](int y) { return d_ck + (size_t)y * srows * n; };
+  auto eck = [&](int y) { return d_eck + (size_t)y * 4 * n; };
   auto fail = [&](int code) { rc = code; };
   do {
     if (hipMalloc(&d_st0, sizeof(float) * srows * n) != hipSuccess ||
         hipMalloc(&d_guess, sizeof(float) * (size_t)L * n) != hipSuccess ||
         hipMalloc(&d_ann_dec, sizeof(float) * (size_t)nyears * rows * n) != hipSuccess ||
         hipMalloc(&d_err0, sizeof(int) * 4 * n) != hipSuccess || hipMalloc(&d_chain, sizeof(int) * (m + 1)) != hipSuccess ||
-        hipMalloc(&d_list, sizeof(int) * (m + 1)) != hipSuccess || hipMalloc(&d_flag, sizeof(int) * (m + 1)) != hipSuccess) {
+        hipMalloc(&d_list, sizeof(int) * (m + 1)) != hipSuccess || hipMalloc(&d_flag, sizeof(int) * (m + 1)) != hipSuccess ||
+        hipMalloc(&d_ck, sizeof(float) * (size_t)nyears * srows * n) != hipSuccess ||
+        hipMalloc(&d_eck, sizeof(int) * (size_t)nyears * 4 * n) != hipSuccess) {
       fail(H9G_ENOMEM);
       break;
     }
@@ -1716,7 +1762,9 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
         break;
       }
       if (hipMemcpyAsync(d_ann_dec + (size_t)y * rows * n, ctx->d_ann, sizeof(float) * rows * n,
-                         hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess)
+                         hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
+          hipMemcpyAsync(ck(y), ctx->d_st, sizeof(float) * srows * n, hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
+          hipMemcpyAsync(eck(y), ctx->d_err, sizeof(int) * 4 * n, hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess)
         fail(H9G_EHIP);
     }
     if (rc) break;
@@ -1739,7 +1787,7 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
         fail(H9G_ESTATE);
         break;
       }
-      const int k = (int)list.size();
+      int k = (int)list.size();
       if (hipMemcpy(d_list, list.data(), sizeof(int) * k, hipMemcpyHostToDevice) != hipSuccess) {
         fail(H9G_EHIP);
         break;
@@ -1750,8 +1798,32 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
         fail(H9G_EHIP);
         break;
       }
-      for (int y = 0; y < nyears && !rc; y++)
-        if (int r = run_year_impl(ctx, slots[y], jyear0 + y, d_list, k, d_ann_dec + (size_t)y * rows * n)) fail(r);
+      rerun_cells += k;
+      for (int y = 0; y < nyears && !rc && k > 0; y++) {
+        if (int r = run_year_impl(ctx, slots[y], jyear0 + y, d_list, k, d_ann_dec + (size_t)y * rows * n)) {
+          fail(r);
+          break;
+        }
+        rerun_cell_years += k;
+        rerun_launches++;
+        // the cells back on their old trajectory leave the re-run
+        h9g_merge_kernel<<<(unsigned)((k + 255) / 256), 256, 0, ctx->sc>>>(
+            k, (int)n, (int)srows, d_list, ctx->d_st, ctx->d_err, ck(y), eck(y), ck(nyears - 1), eck(nyears - 1), d_flag);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(flag.data(), d_flag, sizeof(int) * k, hipMemcpyDeviceToHost, ctx->sc) != hipSuccess ||
+            hipStreamSynchronize(ctx->sc) != hipSuccess) {
+          fail(H9G_EHIP);
+          break;
+        }
+        int kk = 0;
+        for (int j = 0; j < k; j++)
+          if (flag[j]) list[kk++] = list[j];
+        if (kk < k && kk > 0 && hipMemcpy(d_list, list.data(), sizeof(int) * kk, hipMemcpyHostToDevice) != hipSuccess) {
+          fail(H9G_EHIP);
+          break;
+        }
+        k = kk;
+      }
       np++;
     }
     if (rc) break;
@@ -1790,8 +1862,21 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
   (void)hipFree(d_chain);
   (void)hipFree(d_list);
   (void)hipFree(d_flag);
+  (void)hipFree(d_ck);
+  (void)hipFree(d_eck);
+  ctx->dec_stats[0] = np;
+  ctx->dec_stats[1] = rerun_cells;
+  ctx->dec_stats[2] = rerun_cell_years;
+  ctx->dec_stats[3] = rerun_launches;
   if (passes) *passes = np;
   return rc ? rc : src;
+}
+
+int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n) {
+  if (!ctx || !out || n < 1) return H9G_EINVAL;
+  const int m = n < 4 ? n : 4;
+  for (int i = 0; i < m; i++) out[i] = ctx->dec_stats[i];
+  return m;
 }
 
 int h9g_sync(h9g_ctx *ctx) {

@@ -175,6 +175,13 @@ INTERFACE
     INTEGER(C_INT32_T), INTENT(OUT) :: passes
     INTEGER(C_INT) :: h9g_run_decade_ordered
   END FUNCTION
+  FUNCTION h9g_decade_stats (ctx, out, n) BIND(C, NAME='h9g_decade_stats')
+    IMPORT :: C_PTR, C_INT, C_INT64_T
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT64_T), INTENT(OUT) :: out (*)
+    INTEGER(C_INT), VALUE :: n
+    INTEGER(C_INT) :: h9g_decade_stats
+  END FUNCTION
   FUNCTION h9g_get_diagnostics_async (ctx, dev_out, stream) &
            BIND(C, NAME='h9g_get_diagnostics_async')
     IMPORT :: C_PTR, C_INT

@@ -23,6 +23,13 @@ PROGRAM H9_HOST
 ! chosen in the optional namelist file h9gpu.nml (/h9gpu/); nx, ny, nland
 ! override the synthetic grid.
 !
+! cell_order = 1 (default) runs the reference's own order: decade by
+! decade (HYBRID9.f90:93-130), each land cell's first substep of a decade
+! reading the smp its predecessor in (y, x) order left behind (HYDROLOGY.
+! f90:270-275, SHARED.f90:198), through h9g_run_decade_ordered -- bit for
+! bit the reference on one rank.  cell_order = 0: every cell its own smp
+! (h9g_run_year per year, isolated-cell semantics, DESIGN.md §1).
+!
 ! Usage:  h9_host [driver.txt] [h9gpu.nml]
 ! Outputs: <out_dir>/annual.f32 (ncell, 12+L, nyears),
 !          <out_dir>/state_end.f32 (packed state, include/h9g.h) and, on a
@@ -43,9 +50,11 @@ REAL(C_FLOAT) :: zi (0:H9G_LMAX+1)
 ! --- extension namelist ----------------------------------------------------
 CHARACTER (LEN = 512) :: input_mode, case_dir, out_dir, pgf_dir
 INTEGER :: nlayers, grow_on, device, grid, year0, nyears, nc_out, gnx, gny, gnland
+INTEGER :: cell_order
 INTEGER(C_INT64_T) :: seed
 NAMELIST /h9gpu/ input_mode, case_dir, out_dir, nlayers, grow_on, device, &
-                 grid, year0, nyears, seed, pgf_dir, nc_out, gnx, gny, gnland
+                 grid, year0, nyears, seed, pgf_dir, nc_out, gnx, gny, gnland, &
+                 cell_order
 CHARACTER (LEN = 600, KIND = C_CHAR), TARGET :: pgf_file (7)
 TYPE(C_PTR) :: pgf_ptr (7)
 CHARACTER (LEN = *), PARAMETER :: pgf_var (7) = &
@@ -56,16 +65,18 @@ CHARACTER (LEN = 4) :: ydate
 ! --- case.nml of the harness (oracle/ref/h9ref_main.f90) -------------------
 INTEGER :: ncell, state_override, ntrace, trace_cells (64), lclim_mode
 NAMELIST /h9case/ ncell, NISURF, year0, nyears, grow_on, state_override, &
-                  ntrace, trace_cells, lclim_mode
+                  ntrace, trace_cells, lclim_mode, cell_order
 
 TYPE(h9g_config) :: cfg
 TYPE(C_PTR) :: ctx
 INTEGER(C_INT) :: rc
 INTEGER :: L, ndays, iyr, jyear, nt, d0, u, i, nslot, nland, nx, ny
+INTEGER :: dsyr, deyr, ndec, k
+INTEGER(C_INT32_T) :: slots (10), passes
 LOGICAL :: have_driver, have_nml
 CHARACTER (LEN = 512) :: arg
 REAL(C_FLOAT), ALLOCATABLE :: theta_s (:,:), hksat (:,:), bsw (:,:), psi_s (:,:)
-REAL(C_FLOAT), ALLOCATABLE :: Fmax (:), forcing (:,:,:), state (:), annual (:,:)
+REAL(C_FLOAT), ALLOCATABLE :: Fmax (:), forcing (:,:,:), state (:), annual (:,:), annual_dec (:,:,:)
 INTEGER(C_INT64_T), ALLOCATABLE :: gid (:)
 REAL(C_FLOAT), ALLOCATABLE :: lat (:)
 REAL(C_DOUBLE) :: diag (H9G_NDIAG)
@@ -76,7 +87,7 @@ INTEGER :: time_BOY (2300-1860+1)
 !----------------------------------------------------------------------!
 input_mode = 'synth'; case_dir = ''; out_dir = '.'; pgf_dir = '.'
 nlayers = 8; grow_on = 1; device = 0; grid = 1; year0 = 0; nyears = 0
-nc_out = 1; gnx = 0; gny = 0; gnland = 0
+nc_out = 1; gnx = 0; gny = 0; gnland = 0; cell_order = 1
 PATH_output = '.'
 seed = 20161123_C_INT64_T
 NISURF = 48; iDEC_start = 1; iDEC_end = 1
@@ -175,7 +186,7 @@ END DO
 !----------------------------------------------------------------------!
 ! GPU context.
 !----------------------------------------------------------------------!
-nslot = 2
+nslot = MERGE (10, 2, cell_order /= 0)     ! a decade's years at once in the reference's order
 cfg%ncell = ncell
 cfg%nlayers = L
 cfg%nisurf = NISURF
@@ -215,6 +226,30 @@ ALLOCATE (annual (ncell, 12 + L))
 OPEN (NEWUNIT = u, FILE = TRIM (out_dir)//'/annual.f32', ACCESS = 'STREAM', &
       FORM = 'UNFORMATTED', STATUS = 'REPLACE')
 d0 = 1
+IF (cell_order /= 0) THEN
+  ! HYBRID9.f90:93-130: decade by decade (1901-1910, 1911-1920, ...), cut to
+  ! [year0, year0 + nyears); the decade's forcing staged into its slots,
+  ! then the cells run in the reference's order
+  ALLOCATE (annual_dec (ncell, 12 + L, 10))
+  dsyr = year0
+  DO WHILE (dsyr < year0 + nyears)
+    deyr = MIN (1901 + 10 * ((dsyr - 1901) / 10) + 9, year0 + nyears - 1)
+    ndec = deyr - dsyr + 1
+    DO k = 1, ndec
+      slots (k) = k - 1
+      CALL stage (k - 1, dsyr + k - 1, d0)
+      d0 = d0 + time_BOY (dsyr+k-1859) - time_BOY (dsyr+k-1-1859)
+    END DO
+    rc = h9g_run_decade_ordered (ctx, slots, dsyr, ndec, annual_dec, passes)
+    CALL h9g_check_stop (ctx, rc)
+    DO k = 1, ndec
+      annual = annual_dec (:, :, k)
+      CALL year_out (dsyr + k - 1)
+    END DO
+    WRITE (*,'(A,I5,A,I5,A,I3)') ' decade', dsyr, ' -', deyr, ' in cell order: passes', passes
+    dsyr = deyr + 1
+  END DO
+ELSE
 CALL stage (0, year0, d0)
 DO iyr = 1, nyears
   jyear = year0 + iyr - 1
@@ -224,18 +259,10 @@ DO iyr = 1, nyears
   rc = h9g_sync (ctx)
   CALL h9g_check_stop (ctx, rc)
   CALL chk (h9g_get_annual (ctx, annual))
-  WRITE (u) annual
-  IF (nc_out /= 0 .AND. TRIM (input_mode) /= 'case') THEN     ! HYBRID9.f90:503-513
-    WRITE (ydate,'(I4)') jyear
-    CALL chk (h9g_write_axy_nc (TRIM (PATH_output)//'/axy'//ydate//'.nc'//C_NULL_CHAR, nx, ny, L, &
-                                zc, ncell, gid, annual))
-  END IF
-  CALL chk (h9g_get_diagnostics (ctx, diag, C_NULL_PTR))
-  WRITE (*,'(A,I5,A,I8,A,ES12.5,A,ES12.5,A,F9.1,A)') ' year', jyear, ' cells', NINT (diag (1)), &
-        ' mean runoff', diag (2) / MAX (diag (1), 1.0D0), ' mm/s  mean soil water', &
-        diag (3) / MAX (diag (1), 1.0D0), ' mm  (', h9g_last_kernel_ms (ctx), ' ms)'
+  CALL year_out (jyear)
   d0 = d0 + nt
 END DO
+END IF
 CLOSE (u)
 ALLOCATE (state (h9g_state_size (L) * ncell))
 CALL chk (h9g_get_state (ctx, state))
@@ -247,6 +274,21 @@ CALL h9g_destroy (ctx)
 WRITE (*,*) 'H9_HOST completed successfully'
 
 CONTAINS
+
+  ! One year's annual means to annual.f32 and axyYYYY.nc, and its line.
+  SUBROUTINE year_out (y)
+    INTEGER, INTENT(IN) :: y
+    WRITE (u) annual
+    IF (nc_out /= 0 .AND. TRIM (input_mode) /= 'case') THEN     ! HYBRID9.f90:503-513
+      WRITE (ydate,'(I4)') y
+      CALL chk (h9g_write_axy_nc (TRIM (PATH_output)//'/axy'//ydate//'.nc'//C_NULL_CHAR, nx, ny, L, &
+                                  zc, ncell, gid, annual))
+    END IF
+    CALL chk (h9g_get_diagnostics (ctx, diag, C_NULL_PTR))    ! (in cell order: the decade's last year)
+    WRITE (*,'(A,I5,A,I8,A,ES12.5,A,ES12.5,A,F9.1,A)') ' year', y, ' cells', NINT (diag (1)), &
+          ' mean runoff', diag (2) / MAX (diag (1), 1.0D0), ' mm/s  mean soil water', &
+          diag (3) / MAX (diag (1), 1.0D0), ' mm  (', h9g_last_kernel_ms (ctx), ' ms)'
+  END SUBROUTINE year_out
 
   SUBROUTINE chk (r)
     INTEGER(C_INT), INTENT(IN) :: r

@@ -19,8 +19,11 @@
  *                      in READ_PGF.f90 order: tas rlds rsds huss ps pr rhs
  * The fortran/h9_gpu.f90 module binds every entry point with BIND(C).
  *
- * Semantics: bit-identical to the reference for isolated cells (every cell
- * carries its own hidden matric potential smp, SHARED.f90:198).
+ * Semantics: h9g_run_decade_ordered is bit-identical to the reference as
+ * it runs on one rank (its cells in order, the module array smp of
+ * SHARED.f90:198 carried from cell to cell); h9g_run_year runs isolated
+ * cells (every cell carries its own smp), bit-identical to the reference
+ * harness run that way.
  * Threading: one host thread per context; contexts are not re-entrant;
  * one context per GPU.  All calls return 0 on success, a positive
  * H9G_ERR_* code for a reference STOP condition (details via
@@ -154,12 +157,19 @@ int h9g_get_errors(h9g_ctx *ctx, int32_t *rec);
  * h9g_run_year's isolated-cell semantics (every cell its own smp) differ
  * from this by up to ~1e-4 relative after the first decade.
  * Solved on the device: each pass re-runs the decade for the cells whose
- * input smp changed, until none does.  annual: (nyears, 12+L, ncell) host
+ * input smp changed, until none does; a re-run cell leaves the pass at the
+ * first year end where its state equals its previous run's (its later years
+ * are then unchanged, bit for bit).  annual: (nyears, 12+L, ncell) host
  * (may be NULL); passes (may be NULL): decade passes run.  Synchronous;
  * returns 0 or the STOP code of the first failing cell in context order
  * (h9g_last_error, with its year). */
 int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0,
                            int nyears, float *annual, int32_t *passes);
+/* Work of the last h9g_run_decade_ordered: out[0..n) of passes, cells
+ * re-run (summed over the passes), cell-years re-run, and year launches of
+ * the re-runs (a re-run cell leaves at the first year end where its state
+ * is its previous run's again).  Returns the count written (<= 4). */
+int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n);
 
 /* --- LCLIM single-site path (HYBRID9.f90:339-480) ---------------------- */
 /* Runs nday days of the site path for every cell of the context: per

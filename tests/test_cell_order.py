@@ -91,8 +91,10 @@ def test_gpu_cell_order_matches_reference(name):
     assert out["rc"] == 0, out["err"]
     assert same_bits(out["annual"], exp["annual"])
     assert same_bits(out["state"], exp["state"])
+    yrs = [w["rerun_cell_years"] for w in out["work"]]
     print(f"{name}: {meta['ncell']} cells x {meta['nyears']} years bit-identical to the reference's cell order; "
-          f"decade passes {out['passes']}")
+          f"decade passes {out['passes']}, cell-years re-run {yrs}, re-run launches "
+          f"{[w['rerun_launches'] for w in out['work']]}")
 
 
 @pytest.mark.gpu

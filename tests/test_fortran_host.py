@@ -55,21 +55,24 @@ def test_fortran_host_reads_driver_txt(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["c1_10x10", "edge"])
+@pytest.mark.parametrize("name", ["c1_10x10", "edge", "co_c1_30yr"])
 def test_fortran_host_matches_reference_golden(tmp_path, name):
     exe = _build()
     meta, inp, exp = load_golden(name)
     n, L = meta["ncell"], meta["L"]
     st0 = None if inp["state0"] is None else refcase.unpack_state(inp["state0"], n, L)
     case = tmp_path / "case"
+    # co_*: the reference's cell order (case.nml cell_order = 1: the host's
+    # decade loop through h9g_run_decade_ordered); the others isolated cells
     refcase.write_case(case, zi=inp["zi"], params=inp["params"], forcing=inp["forcing"],
                        nisurf=inp["nisurf"], year0=inp["year0"], nyears=inp["nyears"],
-                       grow_on=inp["grow_on"], state0=st0)
+                       grow_on=inp["grow_on"], state0=st0, cell_order=meta["kind"] == "cell_order")
     nml = tmp_path / "h9gpu.nml"
     nml.write_text(f"&h9gpu\n input_mode='case', case_dir='{case}', out_dir='{tmp_path}'\n/\n")
     r = subprocess.run([str(exe), str(tmp_path / "no_driver.txt"), str(nml)], capture_output=True,
                        text=True, timeout=600)
     assert "completed successfully" in r.stdout, r.stdout + r.stderr
+    assert ("in cell order" in r.stdout) == (meta["kind"] == "cell_order")
     ann = np.fromfile(tmp_path / "annual.f32", np.float32).reshape(meta["nyears"], 12 + L, n)
     st = np.fromfile(tmp_path / "state_end.f32", np.float32)
     assert same_bits(ann, exp["annual"])
@@ -105,8 +108,9 @@ def test_fortran_host_pgf_netcdf_mode(tmp_path):
     drv.write_text(f"'{out}'\n48\n.T.\n 1\n 1\n.F.\n .F.\n 'a'\n 'b'\n 1901\n 1902\n 0\n0.0\n0.0\n 1\n 1\n" +
                    "".join(f"{v}\n" for v in synth.ZI_L8[:10]))
     nml = tmp_path / "h9gpu.nml"
+    # isolated cells (cell_order = 0), compared with h9g_run_year below
     nml.write_text(f"&h9gpu\n input_mode='pgf', pgf_dir='{pgf}', out_dir='{tmp_path}', grow_on=1,\n"
-                   f" year0=1901, nyears=2, gnx={nx}, gny={ny}, gnland={nland}\n/\n")
+                   f" year0=1901, nyears=2, gnx={nx}, gny={ny}, gnland={nland}, cell_order=0\n/\n")
     r = subprocess.run([str(exe), str(drv), str(nml)], capture_output=True, text=True, timeout=600)
     assert "completed successfully" in r.stdout, r.stdout + r.stderr
     ann = np.fromfile(tmp_path / "annual.f32", np.float32).reshape(2, 20, nland)
