@@ -105,6 +105,7 @@ def lib() -> C.CDLL:
         "h9g_run_decade_ordered": (C.c_int, [vp, C.POINTER(C.c_int32), C.c_int, C.c_int, _FP,
                                              C.POINTER(C.c_int32)]),
         "h9g_decade_stats": (C.c_int, [vp, C.POINTER(C.c_int64), C.c_int]),
+        "h9g_set_chains": (C.c_int, [vp, C.POINTER(C.c_int32)]),
         "h9g_sync": (C.c_int, [vp]),
         "h9g_last_error": (C.c_int, [vp, C.POINTER(_Error)]),
         "h9g_get_errors": (C.c_int, [vp, C.POINTER(C.c_int32)]),
@@ -359,6 +360,17 @@ class Context:
             raise ReferenceStop(self.last_error())
         return out, int(np_.value)
 
+    def set_chains(self, chain=None):
+        """Independent cell-order chains, one per reference rank
+        (h9g_set_chains; shard.reference_blocks gives the reference's).
+        None: one chain."""
+        if chain is None:
+            _check(self._lib.h9g_set_chains(self._h, None), "h9g_set_chains")
+            return
+        ch = np.ascontiguousarray(chain, dtype=np.int32)
+        assert ch.size == self.ncell
+        _check(self._lib.h9g_set_chains(self._h, ch.ctypes.data_as(C.POINTER(C.c_int32))), "h9g_set_chains")
+
     def decade_stats(self) -> dict:
         """Work of the last run_decade_ordered (h9g_decade_stats)."""
         out = (C.c_int64 * 4)()
@@ -503,14 +515,16 @@ def decades(year0: int, nyears: int):
 
 
 def run_cell_order(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=True,
-                   state0: np.ndarray | None = None, device=0):
+                   state0: np.ndarray | None = None, device=0, chains=None):
     """``run`` in the reference's own cell order: decade by decade through
     ``Context.run_decade_ordered`` (smp carried from cell to cell, cells in
-    the given order).  Returns dict(annual, state, rc, err, errors, passes
-    (per decade), work (decade_stats per decade))."""
+    the given order; chains: a reference rank per cell, each rank its own
+    chain, shard.reference_blocks).  Returns dict(annual, state, rc, err,
+    errors, passes (per decade), work (decade_stats per decade))."""
     L = params["theta_s"].shape[1]
     n = params["fmax"].size
     with Context(n, zi, nlayers=L, nisurf=nisurf, grow_on=grow_on, device=device, nslots=10) as ctx:
+        ctx.set_chains(chains)
         ctx.set_params(params)
         if state0 is None:
             ctx.init_state()

@@ -405,19 +405,22 @@ __global__ void __launch_bounds__(256) h9g_unperm_annual_kernel(int m, int n, in
 // Cell-order mode (h9g_run_decade_ordered).  The reference's cell loop
 // (HYBRID9.f90:120-295) leaves the module array smp (SHARED.f90:198) as the
 // last cell's, and the next cell's first substep reads it in beta
-// (HYDROLOGY.f90:270-275).  Chain position j of m land cells (context
-// order) starts a decade from the smp cell chain[j-1] holds now (for j = 0:
-// what chain[m-1] held when the decade started).  h9g_chain_kernel compares
-// that with the smp the cell last started from (guess, L rows of n), takes
-// it over where it differs and flags the cell for a re-run.
+// (HYDROLOGY.f90:270-275).  The m land cells (context order) form chains,
+// one per reference rank (h9g_set_chains); position j starts a decade from
+// the smp its predecessor pred[j] holds now, or, for a chain's first cell
+// (first[j]), from what the chain's last cell pred[j] held when the decade
+// started.  h9g_chain_kernel compares that with the smp the cell last
+// started from (guess, L rows of n), takes it over where it differs and
+// flags the cell for a re-run.
 __global__ void __launch_bounds__(256) h9g_chain_kernel(int m, int n, int L, const int *__restrict__ chain,
+                                                        const int *__restrict__ pred, const int *__restrict__ first,
                                                         const float *__restrict__ st, const float *__restrict__ st0,
                                                         float *__restrict__ guess, int *__restrict__ flag) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   const int k = chain[j];
-  const float *src = j == 0 ? st0 : st;
-  const int p = j == 0 ? chain[m - 1] : chain[j - 1];
+  const float *src = first[j] ? st0 : st;
+  const int p = pred[j];
   int differ = 0;
   for (int i = 0; i < L; i++) {
     const float v = src[(size_t)(2 * L + i) * n + p];
@@ -425,6 +428,22 @@ __global__ void __launch_bounds__(256) h9g_chain_kernel(int m, int n, int L, con
     guess[(size_t)i * n + k] = v;
   }
   flag[j] = differ;
+}
+
+// Pass 0's input of every chain's first cell: the smp its chain's last cell
+// holds when the decade starts (into the state and the guess).
+__global__ void __launch_bounds__(256) h9g_chain_start_kernel(int m, int n, int L, const int *__restrict__ chain,
+                                                              const int *__restrict__ pred, const int *__restrict__ first,
+                                                              const float *__restrict__ st0, float *__restrict__ st,
+                                                              float *__restrict__ guess) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m || !first[j]) return;
+  const int k = chain[j], p = pred[j];
+  for (int i = 0; i < L; i++) {
+    const float v = st0[(size_t)(2 * L + i) * n + p];
+    st[(size_t)(2 * L + i) * n + k] = v;
+    guess[(size_t)i * n + k] = v;
+  }
 }
 
 // The listed cells back to the decade's starting state (state rows and STOP
@@ -953,6 +972,7 @@ struct h9g_ctx {
   float *d_ann_s = nullptr;       // the year kernel's annual sums in slot order
   unsigned *d_aqbits = nullptr;   // H9G_DUMP_AQ builds: day-level water-table record of the last year
   int64_t dec_stats[4] = {0, 0, 0, 0};   // last h9g_run_decade_ordered (h9g_decade_stats)
+  std::vector<int> chain_id;      // h9g_set_chains: reference rank (block) of every cell; empty = one chain
   int *d_hist = nullptr;          // per cell: substeps of the last year below the column (-1: none)
   int hist_nsub = 0;              // substeps of that year
   unsigned *d_pace = nullptr;     // Pacer mode 2 progress rows (h9g_pair.h)
@@ -1714,9 +1734,34 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
     if (sum > 1.0E-8f && err0h[c] == 0) chain.push_back((int)c);
   }
   const int m = (int)chain.size();
+  // predecessors: the previous land cell of the same chain (h9g_set_chains),
+  // for a chain's first cell its last one (read at the decade's start)
+  std::vector<int> pred(m), first(m);
+  {
+    std::vector<int> last_of, first_of;   // per chain id: position of its last / first land cell
+    auto cid = [&](int j) { return ctx->chain_id.empty() ? 0 : ctx->chain_id[(size_t)chain[j]]; };
+    for (int j = 0; j < m; j++) {
+      const int c = cid(j);
+      if ((int)last_of.size() <= c) {
+        last_of.resize((size_t)c + 1, -1);
+        first_of.resize((size_t)c + 1, -1);
+      }
+      if (last_of[(size_t)c] < 0) {
+        first_of[(size_t)c] = j;
+        first[j] = 1;
+      } else {
+        pred[j] = chain[last_of[(size_t)c]];
+        first[j] = 0;
+      }
+      last_of[(size_t)c] = j;
+    }
+    for (int j = 0; j < m; j++)
+      if (first[j]) pred[j] = chain[last_of[(size_t)cid(j)]];
+  }
   const size_t srows = (size_t)h9g_state_size(L);
   float *d_st0 = nullptr, *d_guess = nullptr, *d_ann_dec = nullptr, *d_ck = nullptr;
   int *d_err0 = nullptr, *d_chain = nullptr, *d_list = nullptr, *d_flag = nullptr, *d_eck = nullptr;
+  int *d_pred = nullptr, *d_first = nullptr;
   int rc = 0, np = 0;
   int64_t rerun_cells = 0, rerun_cell_years = 0, rerun_launches = 0;
   auto ck = [&](int y) { return d_ck + (size_t)y * srows * n; };
@@ -1728,6 +1773,7 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
         hipMalloc(&d_ann_dec, sizeof(float) * (size_t)nyears * rows * n) != hipSuccess ||
         hipMalloc(&d_err0, sizeof(int) * 4 * n) != hipSuccess || hipMalloc(&d_chain, sizeof(int) * (m + 1)) != hipSuccess ||
         hipMalloc(&d_list, sizeof(int) * (m + 1)) != hipSuccess || hipMalloc(&d_flag, sizeof(int) * (m + 1)) != hipSuccess ||
+        hipMalloc(&d_pred, sizeof(int) * (m + 1)) != hipSuccess || hipMalloc(&d_first, sizeof(int) * (m + 1)) != hipSuccess ||
         hipMalloc(&d_ck, sizeof(float) * (size_t)nyears * srows * n) != hipSuccess ||
         hipMalloc(&d_eck, sizeof(int) * (size_t)nyears * 4 * n) != hipSuccess) {
       fail(H9G_ENOMEM);
@@ -1741,20 +1787,19 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
       break;
     }
     if (m > 0) {
-      if (hipMemcpy(d_chain, chain.data(), sizeof(int) * m, hipMemcpyHostToDevice) != hipSuccess) {
+      if (hipMemcpy(d_chain, chain.data(), sizeof(int) * m, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d_pred, pred.data(), sizeof(int) * m, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d_first, first.data(), sizeof(int) * m, hipMemcpyHostToDevice) != hipSuccess) {
         fail(H9G_EHIP);
         break;
       }
-      // pass 0's input of the chain's first cell: what the last one holds now
-      for (int i = 0; i < L; i++)
-        if (hipMemcpyAsync(ctx->d_st + (size_t)(2 * L + i) * n + chain[0], d_st0 + (size_t)(2 * L + i) * n + chain[m - 1],
-                           sizeof(float), hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
-            hipMemcpyAsync(d_guess + (size_t)i * n + chain[0], d_st0 + (size_t)(2 * L + i) * n + chain[m - 1],
-                           sizeof(float), hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess) {
-          fail(H9G_EHIP);
-          break;
-        }
-      if (rc) break;
+      // pass 0's input of every chain's first cell: what its last one holds now
+      h9g_chain_start_kernel<<<(unsigned)((m + 255) / 256), 256, 0, ctx->sc>>>(m, (int)n, L, d_chain, d_pred, d_first,
+                                                                              d_st0, ctx->d_st, d_guess);
+      if (hipGetLastError() != hipSuccess) {
+        fail(H9G_EHIP);
+        break;
+      }
     }
     for (int y = 0; y < nyears && !rc; y++) {   // pass 0: every cell
       if (int r = run_year_impl(ctx, slots[y], jyear0 + y, nullptr, 0, nullptr)) {
@@ -1771,8 +1816,8 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
     np = 1;
     std::vector<int> flag(m), list;
     while (m > 0) {
-      h9g_chain_kernel<<<(unsigned)((m + 255) / 256), 256, 0, ctx->sc>>>(m, (int)n, L, d_chain, ctx->d_st, d_st0, d_guess,
-                                                                        d_flag);
+      h9g_chain_kernel<<<(unsigned)((m + 255) / 256), 256, 0, ctx->sc>>>(m, (int)n, L, d_chain, d_pred, d_first,
+                                                                        ctx->d_st, d_st0, d_guess, d_flag);
       if (hipGetLastError() != hipSuccess ||
           hipMemcpyAsync(flag.data(), d_flag, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->sc) != hipSuccess ||
           hipStreamSynchronize(ctx->sc) != hipSuccess) {
@@ -1860,6 +1905,8 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
   (void)hipFree(d_ann_dec);
   (void)hipFree(d_err0);
   (void)hipFree(d_chain);
+  (void)hipFree(d_pred);
+  (void)hipFree(d_first);
   (void)hipFree(d_list);
   (void)hipFree(d_flag);
   (void)hipFree(d_ck);
@@ -1870,6 +1917,18 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
   ctx->dec_stats[3] = rerun_launches;
   if (passes) *passes = np;
   return rc ? rc : src;
+}
+
+int h9g_set_chains(h9g_ctx *ctx, const int32_t *chain) {
+  if (!ctx) return H9G_EINVAL;
+  if (!chain) {
+    ctx->chain_id.clear();
+    return 0;
+  }
+  for (size_t c = 0; c < ctx->n; c++)
+    if (chain[c] < 0 || chain[c] >= (int32_t)ctx->n) return H9G_EINVAL;
+  ctx->chain_id.assign(chain, chain + ctx->n);
+  return 0;
 }
 
 int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n) {

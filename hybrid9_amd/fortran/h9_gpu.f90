@@ -175,6 +175,12 @@ INTERFACE
     INTEGER(C_INT32_T), INTENT(OUT) :: passes
     INTEGER(C_INT) :: h9g_run_decade_ordered
   END FUNCTION
+  FUNCTION h9g_set_chains (ctx, chain) BIND(C, NAME='h9g_set_chains')
+    IMPORT :: C_PTR, C_INT, C_INT32_T
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT32_T), INTENT(IN) :: chain (*)
+    INTEGER(C_INT) :: h9g_set_chains
+  END FUNCTION
   FUNCTION h9g_decade_stats (ctx, out, n) BIND(C, NAME='h9g_decade_stats')
     IMPORT :: C_PTR, C_INT, C_INT64_T
     TYPE(C_PTR), VALUE :: ctx

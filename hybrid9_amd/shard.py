@@ -24,6 +24,27 @@ def shard_slice(n: int, rank: int, world: int) -> slice:
     return slice(lo, lo + base + (1 if rank < extra else 0))
 
 
+def reference_blocks(gid, nx: int, ny: int, num_procs: int) -> np.ndarray:
+    """The reference rank (MPI block) of every grid id ``gid`` (iy * nx + ix,
+    0-based) for ``num_procs`` ranks, as INIT.f90 assigns them: an
+    nb x nb grid of blocks, nb = NINT(SQRT(num_procs)), of lon_c = nx / nb by
+    lat_c = ny / nb cells (:271-274), numbered along longitude first
+    (:427-444: chunk(x, y), i_block + 1 every lon_c columns, i_block_s + nb
+    every lat_c rows).  Cells past nb * lon_c or nb * lat_c belong to no
+    block (-1): the reference never runs them.  Within a block the
+    reference visits its cells in (y, x) order (HYBRID9.f90:120-121), i.e.
+    ascending grid id, which is the order of synth.land_cells."""
+    g = np.asarray(gid, dtype=np.int64)
+    nb = int(np.rint(np.sqrt(np.float32(num_procs))))
+    if nb < 1:
+        raise ValueError("num_procs must be >= 1")
+    lon_c, lat_c = nx // nb, ny // nb
+    iy, ix = g // nx, g % nx
+    bx, by = ix // lon_c, iy // lat_c
+    r = by * nb + bx
+    return np.where((bx < nb) & (by < nb), r, -1).astype(np.int32)
+
+
 def weak_seed(base_seed: int, rank: int) -> int:
     """Weak scaling: every rank simulates a full land grid with its own seed."""
     return base_seed + rank

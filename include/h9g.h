@@ -146,25 +146,34 @@ int h9g_get_errors(h9g_ctx *ctx, int32_t *rec);
 /* --- the reference's own cell order (HYBRID9.f90:93-130) ---------------- */
 /* Advances every cell through years jyear0 .. jyear0+nyears-1 (the forcing
  * of year jyear0+k in slots[k]) as ONE pass of the reference's decade loop
- * runs them on one rank: the cell loop (:120-295) visits the land cells in
- * context order, and HYDROLOGY's module array smp (SHARED.f90:198) is not
- * per cell, so a land cell's first substep reads in beta (HYDROLOGY.f90:
- * 270-275) the smp its predecessor left behind; the first land cell reads
- * what the last one holds when the call starts (at a fresh start all smp
- * are 0; the reference leaves smp uninitialised, INIT.f90:109).  Call it
- * once per decade of the reference (1901-1910, 1911-1920, ...) with the
- * rank's cells in (y, x) order to reproduce the reference run bit for bit.
+ * runs them on one rank (or on every rank of h9g_set_chains): the cell
+ * loop (:120-295) visits the land cells in context order, and HYDROLOGY's
+ * module array smp (SHARED.f90:198) is not per cell, so a land cell's
+ * first substep reads in beta (HYDROLOGY.f90:270-275) the smp its
+ * predecessor left behind; the first land cell reads what the last one
+ * holds when the call starts (at a fresh start all smp are 0; the
+ * reference leaves smp uninitialised, INIT.f90:109).  Call it once per
+ * decade of the reference (1901-1910, 1911-1920, ...) with the rank's
+ * cells in (y, x) order to reproduce the reference run bit for bit.
  * h9g_run_year's isolated-cell semantics (every cell its own smp) differ
- * from this by up to ~1e-4 relative after the first decade.
- * Solved on the device: each pass re-runs the decade for the cells whose
- * input smp changed, until none does; a re-run cell leaves the pass at the
- * first year end where its state equals its previous run's (its later years
- * are then unchanged, bit for bit).  annual: (nyears, 12+L, ncell) host
- * (may be NULL); passes (may be NULL): decade passes run.  Synchronous;
- * returns 0 or the STOP code of the first failing cell in context order
- * (h9g_last_error, with its year). */
+ * from this by up to 4e-2 relative from the second decade on (DESIGN.md
+ * §2).  Solved on the device: each pass re-runs the decade for the cells
+ * whose input smp changed, until none does; a re-run cell leaves the pass
+ * at the first year end where its state equals its previous run's (its
+ * later years are then unchanged, bit for bit).  annual: (nyears, 12+L,
+ * ncell) host (may be NULL); passes (may be NULL): decade passes run.
+ * Synchronous; returns 0 or the STOP code of the first failing cell in
+ * context order (h9g_last_error, with its year). */
 int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0,
                            int nyears, float *annual, int32_t *passes);
+/* Splits the context's cells into independent chains for
+ * h9g_run_decade_ordered, one per reference MPI rank: chain[c] (ncell
+ * int32, 0 <= id < ncell) is the rank whose block holds cell c (INIT.f90:
+ * 271-274, 427-444; hybrid9_amd.shard.reference_blocks).  Each chain runs
+ * its cells in context order, as that rank runs its block, so a context
+ * holding several ranks' blocks reproduces them all at once.  NULL: one
+ * chain (the default, a one-rank run). */
+int h9g_set_chains(h9g_ctx *ctx, const int32_t *chain);
 /* Work of the last h9g_run_decade_ordered: out[0..n) of passes, cells
  * re-run (summed over the passes), cell-years re-run, and year launches of
  * the re-runs (a re-run cell leaves at the first year end where its state

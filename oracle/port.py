@@ -112,13 +112,15 @@ def decades(year0, nyears):
 
 
 def run_cell_order(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=1,
-                   state0=None):
+                   state0=None, chains=None):
     """The reference's own order (HYBRID9.f90:93-130): decade -> cell ->
     year, with smp (SHARED.f90:198) carried from cell to cell: a land cell's
     first substep of a decade reads the smp its predecessor in cell order
     left behind (HYDROLOGY.f90:270-275); the first land cell reads the smp
-    the last land cell holds when the decade starts.  Restated on the C
-    oracle one (cell, decade) at a time; same contract as run()."""
+    the last land cell holds when the decade starts.  chains: a reference
+    rank per cell (each rank its own chain, its cells in the given order).
+    Restated on the C oracle one (cell, decade) at a time; same contract as
+    run()."""
     L = params["theta_s"].shape[1]
     n = params["fmax"].size
     fo = np.ascontiguousarray(forcing, dtype=np.float32)
@@ -130,20 +132,27 @@ def run_cell_order(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow
     land =[c for c in range(n) if _mask_sum(params["theta_s"][c]) > np.float32(1.0e-8)]
     one = lambda a, c: a[c:c + 1]  # noqa: E731
     rc, err = 0, dict(code=0, cell=-1, day=-1, substep=-1, value=0.0)
+    cid = np.zeros(n, np.int64) if chains is None else np.asarray(chains, np.int64)
+    groups = [[c for c in land if cid[c] == r] for r in sorted(set(cid[land].tolist()))]
     day0 = 0
     for y0, ny in decades(year0, nyears):
         nd = sum(_days(y0 + k) for k in range(ny))
-        carry = st["smp"][land[-1]].copy() if land else None
+        carry = {}
+        for grp in groups:
+            carry[grp[0]] = st["smp"][grp[-1]].copy()     # the chain's first cell: its last one's smp
+        prev = {}
+        for grp in groups:
+            for a_, b_ in zip(grp, grp[1:]):
+                prev[b_] = a_
         for c in land:
             s1 = {k: one(v, c).copy() for k, v in st.items()}
-            s1["smp"][0] = carry
+            s1["smp"][0] = carry[c] if c in carry else st["smp"][prev[c]].copy()
             r = run(zi=zi, params={k: one(v, c) for k, v in params.items()},
                     forcing=np.ascontiguousarray(fo[:, day0:day0 + nd, c:c + 1]), nisurf=nisurf,
                     year0=y0, nyears=ny, grow_on=grow_on, state0=s1)
             for k in st:
                 st[k][c] = r["state"][k][0]
             ann[y0 - year0:y0 - year0 + ny, :, c] = r["annual"][:, :, 0]
-            carry = st["smp"][c].copy()
             if r["rc"] and not rc:
                 rc = r["rc"]
                 err = dict(r["err"], cell=c)

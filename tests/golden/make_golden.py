@@ -396,6 +396,47 @@ def cell_order_case(name, gid, *, year0=1901, nyears=30, nisurf=48, grow_on=1, s
           f"{(OUT / f'{name}.npz').stat().st_size / 1e3:.0f} kB")
 
 
+def cell_order_blocks_case(name, gid, nx, ny, num_procs, *, year0=1901, nyears=20, nisurf=48, grow_on=1):
+    """The reference on num_procs MPI ranks: the cells gid (row-major ids of
+    an nx x ny grid, ascending) cut into the reference's blocks
+    (shard.reference_blocks, INIT.f90:271-274,427-444), every block run by
+    its own h9ref process in cell order -- ranks never communicate, so each
+    is one independent chain (HYBRID9.f90:120-295)."""
+    from hybrid9_amd.shard import reference_blocks
+    gid = np.asarray(gid, dtype=np.int64)
+    p, f = synth_inputs(gid, year0, nyears)
+    L = 8
+    loc = (gid // synth.NX05 - gid[0] // synth.NX05) * nx + (gid % synth.NX05 - gid[0] % synth.NX05)
+    rank = reference_blocks(loc, nx, ny, num_procs)
+    assert (rank >= 0).all() and np.all(np.diff(loc) > 0)
+    ann = np.full((nyears, 12 + L, gid.size), np.nan, np.float32)
+    st = {}
+    for r in sorted(set(rank.tolist())):
+        sel = np.where(rank == r)[0]
+        out = refcase.run_case(cell_order=True, zi=synth.ZI_L8, params={k: v[sel] for k, v in p.items()},
+                               forcing=np.ascontiguousarray(f[:, :, sel]), nisurf=nisurf, year0=year0,
+                               nyears=nyears, grow_on=grow_on)
+        ann[:, :, sel] = out["annual"]
+        for k, v in out["state"].items():
+            st.setdefault(k, np.zeros((gid.size,) + v.shape[1:], v.dtype))[sel] = v
+    one = refcase.run_case(cell_order=True, zi=synth.ZI_L8, params=p, forcing=f, nisurf=nisurf, year0=year0,
+                           nyears=nyears, grow_on=grow_on)["annual"]
+    fields = refcase.annual_fields(L)
+    pick = [fields.index(k) for k in ["rnf", "theta_total"] + [f"theta{i + 1}" for i in range(L)]]
+    vs_one = dict(annual=rel_bound(ann[:, pick, :], one[:, pick, :]),
+                  cells_differing=int(np.any(np.any(ann.view(np.uint32) != one.view(np.uint32), axis=0),
+                                             axis=0).sum()))
+    meta = dict(name=name, kind="cell_order", seed=synth.SEED, gid=gid.tolist(), L=L, ncell=int(gid.size),
+                year0=year0, nyears=nyears, nisurf=nisurf, grow_on=grow_on, zi=synth.ZI_L8.tolist(),
+                input_sha256=digest(packed_params(p), f), grid=[nx, ny], num_procs=num_procs,
+                rank=rank.tolist(), blocks_vs_one_rank=vs_one,
+                generator="oracle/_ref/h9ref cell_order=1, one process per reference block "
+                          "(reference HYDROLOGY.f90/GROW.f90, amdflang -O2)")
+    np.savez_compressed(OUT / f"{name}.npz", meta=np.array(json.dumps(meta)), annual=ann,
+                        state=refcase.pack_state(st, L))
+    print(f"{name}: {gid.size} cells in {len(set(rank.tolist()))} blocks x {nyears} yr, vs one rank {vs_one}")
+
+
 def main_cell_order():
     g10 = np.array([(80 + j) * synth.NX05 + 400 + i for j in range(10) for i in range(10)])
     # config 1's grid over three decades (1901-1930)
@@ -404,6 +445,8 @@ def main_cell_order():
     land = synth.land_cells()
     rows = land // synth.NX05
     cell_order_case("co_band", land[(rows >= 150) & (rows < 158)], nyears=20)
+    # config 1's grid as the reference runs it on 4 MPI ranks (2 x 2 blocks of 5 x 5)
+    cell_order_blocks_case("co_c1_blocks4", g10, 10, 10, 4)
 
 
 def site_inputs(gid, L, nisurf, years, events, seed=synth.SEED, soils="synth", ppt_scale=1.0):

@@ -64,6 +64,51 @@ def test_reference_depends_on_its_rank_split():
     assert two["cells_differing"] >= 1 and two["annual"] > 1e-6
 
 
+def test_reference_blocks_follow_init():
+    """shard.reference_blocks against a loop restating INIT.f90:271-274 and
+    the chunk assignment of :427-444 (1-based x, y; ids along longitude)."""
+    from hybrid9_amd.shard import reference_blocks
+    for nx, ny, P in ((10, 10, 4), (720, 360, 4), (720, 360, 9), (720, 360, 16), (12, 6, 9), (7, 5, 1)):
+        nb = int(round(np.sqrt(P)))
+        lon_c, lat_c = nx // nb, ny // nb
+        chunk = np.full((ny, nx), -1)
+        i_block_s = 0
+        for y in range(1, ny + 1):
+            i_block = i_block_s
+            for x in range(1, nx + 1):
+                chunk[y - 1, x - 1] = i_block
+                if x % lon_c == 0:
+                    i_block += 1
+            if y % lat_c == 0:
+                i_block_s += nb
+        # cells outside the nb x nb blocks are never run by the reference
+        run = np.zeros((ny, nx), bool)
+        run[:nb * lat_c, :nb * lon_c] = True
+        want = np.where(run, chunk, -1).ravel()
+        assert np.array_equal(reference_blocks(np.arange(nx * ny), nx, ny, P), want), (nx, ny, P)
+
+
+def test_blocks_golden_records_the_rank_dependence():
+    """The reference's result depends on its decomposition: the 4-rank run
+    of config 1's grid differs from the 1-rank run (recorded by make_golden
+    from the reference itself)."""
+    meta, _, _ = load_golden("co_c1_blocks4")
+    rec = meta["blocks_vs_one_rank"]
+    assert meta["num_procs"] == 4 and len(set(meta["rank"])) == 4
+    assert rec["cells_differing"] >= 1
+
+
+@pytest.mark.slow
+def test_oracle_cell_order_blocks_match_reference_golden():
+    """oracle.port.run_cell_order with one chain per reference block,
+    bit for bit against the reference's 4-process run."""
+    from oracle import port
+    meta, inp, exp = load_golden("co_c1_blocks4")
+    out = port.run_cell_order(chains=np.asarray(meta["rank"]), **inp)
+    assert out["rc"] == 0
+    assert same_bits(out["annual"], exp["annual"])
+
+
 @pytest.mark.slow
 def test_oracle_cell_order_matches_reference_golden():
     """oracle.port.run_cell_order restates the reference's order on the C
@@ -95,6 +140,33 @@ def test_gpu_cell_order_matches_reference(name):
     print(f"{name}: {meta['ncell']} cells x {meta['nyears']} years bit-identical to the reference's cell order; "
           f"decade passes {out['passes']}, cell-years re-run {yrs}, re-run launches "
           f"{[w['rerun_launches'] for w in out['work']]}")
+
+
+@pytest.mark.gpu
+def test_gpu_cell_order_blocks_match_reference():
+    """One context holding the 4 reference ranks' blocks as 4 chains
+    (h9g_set_chains) reproduces the reference's 4-process run bit for bit;
+    so does each rank's block run alone (one GPU per rank)."""
+    import hybrid9_amd as h
+    meta, inp, exp = load_golden("co_c1_blocks4")
+    rank = np.asarray(meta["rank"])
+    out = h.run_cell_order(chains=rank, **inp)
+    assert out["rc"] == 0, out["err"]
+    assert same_bits(out["annual"], exp["annual"])
+    assert same_bits(out["state"], exp["state"])
+    from oracle import refcase
+    L, n = meta["L"], meta["ncell"]
+    ex_st = refcase.unpack_state(exp["state"], n, L)
+    for r in (0, 3):                        # two of the ranks, each on its own context
+        sel = np.where(rank == r)[0]
+        sub = dict(inp, params={k: v[sel] for k, v in inp["params"].items()},
+                   forcing=np.ascontiguousarray(inp["forcing"][:, :, sel]))
+        o = h.run_cell_order(**sub)
+        assert o["rc"] == 0
+        assert same_bits(o["annual"], exp["annual"][:, :, sel])
+        got = refcase.unpack_state(o["state"], sel.size, L)
+        assert all(same_bits(got[k], ex_st[k][sel]) for k in got)
+    print(f"co_c1_blocks4: 4 reference ranks as chains: bit-identical; passes {out['passes']}")
 
 
 @pytest.mark.gpu

@@ -17,4 +17,9 @@ echo "== driver bench" && timeout -k 10 300 python -u bench.py --gpus 1 --steps 
 rc=$?; tail -c 800 gpurun_out/bench_${TAG}_driver.log; [ $rc -eq 0 ] || exit $rc
 echo "== cell-order bench" && timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 10 --order cell \
   --no-cpu-baseline > gpurun_out/bench_${TAG}_cellorder.log 2>&1
-rc=$?; tail -c 1500 gpurun_out/bench_${TAG}_cellorder.log; exit $rc
+rc=$?; tail -c 1500 gpurun_out/bench_${TAG}_cellorder.log; [ $rc -eq 0 ] || exit $rc
+if [ -f hybrid9_amd/lib/libh9g_aq.so ]; then     # day-level water-table record (tools/aq_sort.py)
+  echo "== aq dump" && H9G_LIB=hybrid9_amd/lib/libh9g_aq.so H9G_AQ_DUMP=gpurun_out/aq_$TAG.bin timeout -k 10 300 \
+    python -u bench.py --steps 8 --warmup 0 --no-cpu-baseline > gpurun_out/bench_${TAG}_aq.log 2>&1
+  rc=$?; tail -c 300 gpurun_out/bench_${TAG}_aq.log; exit $rc
+fi
