@@ -415,6 +415,28 @@ def ordered_years(ctx, pl: dict, s0: int, s1: int, exchange, work: list) -> None
             exchange()
 
 
+def cell_order_line(ctx, pl: dict, ns: int, sync) -> dict:
+    """The same cells in the reference's own cell order (h9g_run_decade_ordered),
+    after the main measurement: the state re-initialised, decade 1901-1910
+    untimed, decade 1911-1920 timed (steps 0-19 of the ring).  A secondary
+    line: the main `value` is the isolated-cell path."""
+    from hybrid9_amd import synth
+    ctx.init_state()
+    sub = dict(pl, W=10, K=10, years=pl["years"][:20], slot_of_step=pl["slot_of_step"][:20])
+    work = []
+    el = timed_steps(ctx, sub, None, sync, "cell", work)
+    kern_ms = ctx.total_kernel_ms(reset=True)
+    d = ctx.get_diagnostics()
+    failed = int(round(float(d[11])))
+    steps = sum(synth.days_in_year(y) for y in sub["years"][10:]) * ns
+    n = pl["gid"].size
+    return {"value": (n - failed) * steps / el, "unit": "cell-steps/s", "years": "1911-1920 timed (1901-1910 untimed)",
+            "ms_per_year": el / 10 * 1e3, "kernel_ms_per_year": kern_ms / 10, "decades": work,
+            "rerun_cell_years_per_cell_year": sum(w["rerun_cell_years"] for w in work) / float(n * 10),
+            "semantics": "the reference's decade -> cell -> year order, smp carried from cell to cell "
+                         "(bit-identical to the reference on one rank, DESIGN.md §2)"}
+
+
 def timed_steps(ctx, pl: dict, exchange, sync, order: str = "isolated", work: list | None = None) -> float:
     """W untimed warmup years, then K timed years between two `sync`s
     (barrier + device synchronisation).  Returns the elapsed seconds.
@@ -463,6 +485,10 @@ def main():
                     help="cell: the reference's own cell order (h9g_run_decade_ordered per decade, smp "
                          "carried from cell to cell, bit-identical to the reference); isolated: every cell "
                          "its own smp (h9g_run_year per year)")
+    ap.add_argument("--no-cell-order-line", action="store_true",
+                    help="skip the secondary measurement of the reference's cell order (the default run "
+                         "adds it at N=1 when the ring holds 1901-1920: decade 1901-1910 untimed, "
+                         "1911-1920 timed, reported under cell_order, never as `value`)")
     ap.add_argument("--forcing", choices=["device", "nc4"], default="device",
                     help="nc4: every step's forcing is read from synthetic PGF netCDF-4 files through "
                          "h9g_nc_forcing_prefetch (ingest-inclusive; DESIGN.md, never as `value`)")
@@ -602,6 +628,9 @@ def main():
         out["cell_order"] = {"decades": work,
                              "rerun_cell_years_per_cell_year": sum(w["rerun_cell_years"] for w in work) /
                              max(1.0, float(gid.size * K))}
+    elif (world == 1 and host_fed is None and nc_fed is None and not args.no_cell_order_line
+          and len(pl["years"]) >= 20):
+        out["cell_order"] = cell_order_line(ctx, pl, ns, sync)
     if host_fed is not None:
         out["host_fed"] = host_fed.describe()
         host_fed.close()
