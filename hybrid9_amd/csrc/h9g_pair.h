@@ -90,6 +90,9 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
 #ifndef H9G_SPARE_L10
 #define H9G_SPARE_L10 0   // spare lanes in the 3-wave L = 10 build too (PairStore::kSpare)
 #endif
+#ifndef H9G_SPARE_SLOT0
+#define H9G_SPARE_SLOT0 0   // spare lanes take the pairs' first slot instead of their last (hydrology_pair)
+#endif
 
 template <int K>
 struct FV {
@@ -1092,6 +1095,9 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
       // either side re-runs the pair lane's slots exactly, as in par_d.
       constexpr int S = CS::LANES, NSP = 64 - S, QS = (S + NSP - 1) / NSP;   // QS: rounds with spare work
       static_assert(QS <= NT - 1, "the spare lanes cover the last slot in NT - 1 rounds");
+      // the slot the spare lanes take (SPS) and the pairs' slot of round q
+      constexpr int SPS = H9G_SPARE_SLOT0 ? 0 : NT - 1;
+      auto ps = [](int q) constexpr { return SPS == 0 ? q + 1 : q; };
       const bool st = sp.spare;
       const int hh = sp.h;
       auto kq = [&](int q) __attribute__((always_inline)) {   // spare lane: the pair lane of round q
@@ -1125,17 +1131,17 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
 #pragma unroll
         for (int q = 0; q < NT - 1; q++) {
           const int k = kq(q);
-          const lds_float *o = st ? cs.wb + k + (NT - 1) * S : cs.self + q * S;
+          const lds_float *o = st ? cs.wb + k + SPS * S : cs.self + ps(q) * S;
           const float zwq = kPre ? zwk[q < QS ? q : QS - 1] : lane_get(zwtmm, k);   // in every lane (below)
           bool b = false;
-          r[q] = eq_body(st ? L - 1 + (k & 1) : 2 * q + 1 + hh,
-                         [&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
-                         st ? zwq : zwtmm, b);
-          rv[q] = r[q].v[0];
+          r[ps(q)] = eq_body(st ? 2 * SPS + 1 + (k & 1) : 2 * ps(q) + 1 + hh,
+                             [&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
+                             st ? zwq : zwtmm, b);
+          rv[q] = r[ps(q)].v[0];
           fl |= (b ? 1 : 0) << q;
           if ((H9G_SPARE_FENCE >> q) & 1) sched_fence();
         }
-        r[NT - 1].v[0] = back(rv);
+        r[SPS].v[0] = back(rv);
         const int gf = lane_geti(fl, src);
         const bool bad = !st & ((fl | ((gf >> qo) & 1)) != 0);
         if (__builtin_expect(bad, 0)) {
@@ -1147,7 +1153,9 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
       }
       pr.mark(2);
       {
-        const float th_l = sel(hh, theta[L - 1], theta[L]), thp_l = theta[L];   // this lane's last-slot operands
+        // this lane's operands of slot SPS (theta(i), theta(ip), ip = min(i + 1, L))
+        const float th_l = sel(hh, theta[2 * SPS + 1], theta[2 * SPS + 2]);
+        const float thp_l = sel(hh, theta[2 * SPS + 2], theta[2 * SPS + 3 <= L ? 2 * SPS + 3 : L]);
         float thk[QS], thpk[QS];
         if constexpr (kPre) {
 #pragma unroll
@@ -1162,13 +1170,20 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
 #pragma unroll
         for (int q = 0; q < NT - 1; q++) {
           const int k = kq(q), qq = q < QS ? q : QS - 1;
-          const lds_float *o = st ? cs.wb + k + (NT - 1) * S : cs.self + q * S;
-          const lds_float *pt = st ? cs.wb + (k | 1) + (PF_TS * NT + NT - 1) * S : pe + q * S;
+          const int t = ps(q);
+          const lds_float *o = st ? cs.wb + k + SPS * S : cs.self + t * S;
+          // TS(ip) of the slot: layer 2t+2 (odd column, row t) for the even
+          // lane, 2t+3 (even column, row t+1) for the odd one; TS(L) (odd
+          // column, row NT-1) in the last slot
+          const lds_float *pt_sp = SPS == NT - 1 ? cs.wb + (k | 1) + (PF_TS * NT + NT - 1) * S
+                                                 : cs.wb + ((k & 1) ? (k & ~1) + S : (k | 1)) + (PF_TS * NT + SPS) * S;
+          const lds_float *pt_own = t == NT - 1 ? cs.even + 1 + (PF_TS * NT + NT - 1) * S : pe + t * S;
+          const lds_float *pt = st ? pt_sp : pt_own;
           const float thq = kPre ? thk[qq] : lane_get(th_l, k), thpq = kPre ? thpk[qq] : lane_get(thp_l, k);
           bool b = false;
-          r[q] = hk_body([&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
-                         st ? thq : sel(hh, theta[2 * q + 1], theta[2 * q + 2]),
-                         st ? thpq : sel(hh, theta[2 * q + 2], theta[2 * q + 3]), *pt, b);
+          r[t] = hk_body([&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
+                         st ? thq : sel(hh, theta[2 * t + 1], theta[2 * t + 2]),
+                         st ? thpq : sel(hh, theta[2 * t + 2], theta[2 * t + 3 <= L ? 2 * t + 3 : L]), *pt, b);
           fl |= (b ? 1 : 0) << q;
           if ((H9G_SPARE_FENCE >> q) & 1) sched_fence();
         }
@@ -1176,8 +1191,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
         for (int kk = 0; kk < 4; kk++) {
           float rv[NT - 1];
 #pragma unroll
-          for (int q = 0; q < NT - 1; q++) rv[q] = r[q].v[kk];
-          r[NT - 1].v[kk] = back(rv);
+          for (int q = 0; q < NT - 1; q++) rv[q] = r[ps(q)].v[kk];
+          r[SPS].v[kk] = back(rv);
         }
         const int gf = lane_geti(fl, src);
         const bool bad = !st & ((fl | ((gf >> qo) & 1)) != 0);
