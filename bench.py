@@ -302,6 +302,7 @@ class NcFed:
         t = time.perf_counter()
         h.nc_forcing_read(self.paths, self.nx, self.ny, np.asarray(gid, np.int64), 0, 365)
         self.read_s = time.perf_counter() - t
+        self.read_stages = h.nc_read_stats()           # h9g_nc_read_stats of that read
 
     def step(self, s):
         from hybrid9_amd import synth
@@ -318,7 +319,7 @@ class NcFed:
         import hybrid9_amd as h
         return {"source": "synthetic PGF v2.1 netCDF-4 files (one chunk per day, shuffle + deflate 4)",
                 "file_bytes_per_year": int(self.bytes), "write_s": self.write_s,
-                "read_s_per_year_sync": self.read_s,
+                "read_s_per_year_sync": self.read_s, "read_stages": self.read_stages,
                 "io_threads": int(os.environ.get("H9G_IO_THREADS", "0")) or min(16, os.cpu_count() or 1),
                 "slots": 2, "reader": "h9g_nc_forcing_prefetch (direct chunk reads, libdeflate, host pool)"}
 

@@ -373,10 +373,10 @@ class Context:
 
     def decade_stats(self) -> dict:
         """Work of the last run_decade_ordered (h9g_decade_stats)."""
-        out = (C.c_int64 * 4)()
-        _check(self._lib.h9g_decade_stats(self._h, out, 4), "h9g_decade_stats")
+        out = (C.c_int64 * 64)()
+        m = _check(self._lib.h9g_decade_stats(self._h, out, 64), "h9g_decade_stats")
         return dict(passes=int(out[0]), rerun_cells=int(out[1]), rerun_cell_years=int(out[2]),
-                    rerun_launches=int(out[3]))
+                    rerun_launches=int(out[3]), launch_cells=[int(out[i]) for i in range(4, m)])
 
     def run_site(self, sub, daily, lai, raise_on_stop: bool = True) -> np.ndarray:
         """LCLIM site path (HYBRID9.f90:339-480) over nday days, synchronous.

@@ -973,6 +973,7 @@ struct h9g_ctx {
   unsigned *d_aqbits = nullptr;   // H9G_DUMP_AQ builds: day-level water-table record of the last year
   int64_t dec_stats[4] = {0, 0, 0, 0};   // last h9g_run_decade_ordered (h9g_decade_stats)
   std::vector<int> chain_id;      // h9g_set_chains: reference rank (block) of every cell; empty = one chain
+  std::vector<int64_t> dec_launches;   // last h9g_run_decade_ordered: cells of each re-run launch
   int *d_hist = nullptr;          // per cell: substeps of the last year below the column (-1: none)
   int hist_nsub = 0;              // substeps of that year
   unsigned *d_pace = nullptr;     // Pacer mode 2 progress rows (h9g_pair.h)
@@ -1764,6 +1765,7 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
   int *d_pred = nullptr, *d_first = nullptr;
   int rc = 0, np = 0;
   int64_t rerun_cells = 0, rerun_cell_years = 0, rerun_launches = 0;
+  std::vector<int64_t> launch_cells;   // cells of each re-run launch, in order
   auto ck = [&](int y) { return d_ck + (size_t)y * srows * n; };
   auto eck = [&](int y) { return d_eck + (size_t)y * 4 * n; };
   auto fail = [&](int code) { rc = code; };
@@ -1851,6 +1853,7 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
         }
         rerun_cell_years += k;
         rerun_launches++;
+        launch_cells.push_back(k);
         // the cells back on their old trajectory leave the re-run
         h9g_merge_kernel<<<(unsigned)((k + 255) / 256), 256, 0, ctx->sc>>>(
             k, (int)n, (int)srows, d_list, ctx->d_st, ctx->d_err, ck(y), eck(y), ck(nyears - 1), eck(nyears - 1), d_flag);
@@ -1915,6 +1918,7 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int n
   ctx->dec_stats[1] = rerun_cells;
   ctx->dec_stats[2] = rerun_cell_years;
   ctx->dec_stats[3] = rerun_launches;
+  ctx->dec_launches = launch_cells;
   if (passes) *passes = np;
   return rc ? rc : src;
 }
@@ -1933,8 +1937,9 @@ int h9g_set_chains(h9g_ctx *ctx, const int32_t *chain) {
 
 int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n) {
   if (!ctx || !out || n < 1) return H9G_EINVAL;
-  const int m = n < 4 ? n : 4;
-  for (int i = 0; i < m; i++) out[i] = ctx->dec_stats[i];
+  int m = 0;
+  for (; m < n && m < 4; m++) out[m] = ctx->dec_stats[m];
+  for (size_t i = 0; m < n && i < ctx->dec_launches.size(); i++) out[m++] = ctx->dec_launches[i];
   return m;
 }
 

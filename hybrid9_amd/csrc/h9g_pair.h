@@ -91,7 +91,9 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
 #define H9G_SPARE_L10 0   // spare lanes in the 3-wave L = 10 build too (PairStore::kSpare)
 #endif
 #ifndef H9G_SPARE_SLOT0
-#define H9G_SPARE_SLOT0 0   // spare lanes take the pairs' first slot instead of their last (hydrology_pair)
+// spare lanes take the pairs' first slot instead of their last
+// (hydrology_pair; round 5: 186.5 -> 183.7 ms)
+#define H9G_SPARE_SLOT0 1
 #endif
 
 template <int K>
@@ -1095,7 +1097,13 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
       // either side re-runs the pair lane's slots exactly, as in par_d.
       constexpr int S = CS::LANES, NSP = 64 - S, QS = (S + NSP - 1) / NSP;   // QS: rounds with spare work
       static_assert(QS <= NT - 1, "the spare lanes cover the last slot in NT - 1 rounds");
-      // the slot the spare lanes take (SPS) and the pairs' slot of round q
+      // the slot the spare lanes take (SPS) and the pairs' slot of round q.
+      // SPS = 0 (round 5): the water table lies in layers L-1 or L in most
+      // columns, and the equilibrium profile's in-layer case (a wave-uniform
+      // branch of ~20 VALU on the round's critical path, :530-543) then runs
+      // in the one round where the pairs evaluate their last slot, not in
+      // every round that holds a spare lane's last slot of another pair
+      // (branch counts: entered in 1.77 of 3 rounds with SPS = NT - 1)
       constexpr int SPS = H9G_SPARE_SLOT0 ? 0 : NT - 1;
       auto ps = [](int q) constexpr { return SPS == 0 ? q + 1 : q; };
       const bool st = sp.spare;

@@ -177,7 +177,8 @@ int h9g_set_chains(h9g_ctx *ctx, const int32_t *chain);
 /* Work of the last h9g_run_decade_ordered: out[0..n) of passes, cells
  * re-run (summed over the passes), cell-years re-run, and year launches of
  * the re-runs (a re-run cell leaves at the first year end where its state
- * is its previous run's again).  Returns the count written (<= 4). */
+ * is its previous run's again), then the cells of each re-run launch in
+ * order.  Returns the count written (<= 4 + launches). */
 int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n);
 
 /* --- LCLIM single-site path (HYBRID9.f90:339-480) ---------------------- */

@@ -19,7 +19,7 @@ if [ "$2" != "skip-tests" ]; then
 fi
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-ARGS="--steps 20 --warmup 5 --no-cpu-baseline"
+ARGS="--steps 20 --warmup 5 --no-cpu-baseline --no-cell-order-line"
 run() { # dir name, bench args, rocprof args...
   local name=$1 bargs=$2; shift 2
   echo "== $name"
