@@ -120,12 +120,14 @@ __device__ __forceinline__ void load_tabs(uint64_t *e2, double *l2) {
 template <int L>
 constexpr int pair_waves() { return pair_resident<L>(); }
 
-template <int L, class G, int R>
+// C: columns (pairs) per wave: 22 (h9g_pair_kernel, h9g_pair2_kernel) or 11
+// (h9g_pair11_kernel: 42 helper lanes, 2 rounds per phase at L = 10).
+template <int L, class G, int R, int C = H9G_PCPW>
 __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
-  typedef PairStore<L, H9G_PLANES, R> PS;
+  typedef PairStore<L, 2 * C, R> PS;
   __shared__ uint64_t s_e2[32];
   __shared__ double s_l2[32];
-  __shared__ float s_cell[H9G_PWAVES][PS::ROWS * H9G_PLANES];   // [wave][row][lane]
+  __shared__ float s_cell[H9G_PWAVES][PS::ROWS * 2 * C];   // [wave][row][lane]
   __shared__ float s_zt[zt_size<L>()];
   // the day snapshot addresses its global block by LDS byte offset
   // (PairStore::svw): every static LDS address must lie inside GBLOCK
@@ -143,13 +145,13 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   // carried in registers.  Lanes 12..31 because an LDS read's lanes 32..63
   // share one cycle (bank = dword mod 32): their columns' banks are the 20
   // that pair lanes 32..43 leave free, so a mirrored read adds no conflict.
-  const bool spare = lane >= H9G_PLANES;
+  const bool spare = lane >= 2 * C;
   if (spare && !PS::kSpare) return;
   const int h = lane & 1;
-  const int slot0 = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * H9G_PCPW;
-  const int ncol = min(H9G_PCPW, a.cend - slot0);
+  const int slot0 = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * C;
+  const int ncol = min(C, a.cend - slot0);
   if (ncol <= 0) return;             // an empty wave
-  const int pl = spare ? (lane - H9G_PLANES + 12) % (2 * ncol) : lane;
+  const int pl = spare ? (lane - 2 * C + (C == H9G_PCPW ? 12 : 0)) % (2 * ncol) : lane;
   const int slot = slot0 + (pl >> 1);
   if (slot >= a.cend) return;        // both lanes of a pair leave together
   const int c = a.perm ? a.perm[slot] : slot;
@@ -266,6 +268,20 @@ template <int L, class G>
 __global__ void __launch_bounds__(64 * H9G_PWAVES) __attribute__((amdgpu_waves_per_eu(2, 2)))
 h9g_pair2_kernel(const KArgs a, const G g) {
   pair_body<L, G, 2>(a, g);
+}
+
+// The pair kernel with 11 columns per wave (round 5): the 42
+// lanes past the pairs help in the per-layer phases, which then take 2
+// rounds instead of 5 at L = 10 (hydrology_pair helpers), and the wave's LDS
+// block halves, so every reciprocal field fits at 3 waves per SIMD.  Twice
+// the waves of 22-column ones for the same cells: l10_kind takes it for
+// shards whose 11-column waves still fit one round of 3 per SIMD (the
+// 8-GPU config-5 shard, 33,750 cells: 3,069 waves for 3,072 slots).
+#define H9G_PCPW11 11
+template <int L, class G>
+__global__ void __launch_bounds__(64 * H9G_PWAVES) __attribute__((amdgpu_waves_per_eu(3, 3)))
+h9g_pair11_kernel(const KArgs a, const G g) {
+  pair_body<L, G, 3, H9G_PCPW11>(a, g);
 }
 
 
@@ -1080,6 +1096,7 @@ static GeoKind geo_kind(const h9g_config &c) {
 #if defined(H9G_ISA_L10)
 template __global__ void h9g_pair_kernel<10, GeoC<10, 24>>(const KArgs, const GeoC<10, 24>);
 template __global__ void h9g_pair2_kernel<10, GeoC<10, 24>>(const KArgs, const GeoC<10, 24>);
+template __global__ void h9g_pair11_kernel<10, GeoC<10, 24>>(const KArgs, const GeoC<10, 24>);
 #else
 template __global__ void h9g_pair_kernel<8, GeoC<8, 48>>(const KArgs, const GeoC<8, 48>);
 #endif
@@ -1169,7 +1186,7 @@ static int l10_kind(size_t n, int ncu, size_t *n_solo) {
 size_t h9g_config_bytes(const h9g_config *cfg) {
   if (!cfg || cfg->ncell <= 0 || cfg->nlayers < 1 || cfg->max_days < 1 || cfg->nslots < 1) return 0;
   const size_t n = (size_t)cfg->ncell, L = (size_t)cfg->nlayers;
-  const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
+  const size_t per_block = (size_t)H9G_PCPW11 * H9G_PWAVES;   // (the smallest workgroup: kind 5)
   // + the slot-ordered copies of a forcing slot and of the annual sums
   // (h9g_run_year, allocated on first use)
   return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * ((size_t)cfg->nslots + 1) +
@@ -1278,7 +1295,7 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     h9g_destroy(ctx);
     return nullptr;
   }
-  static const char *names[5][2][3] = {
+  static const char *names[6][2][3] = {
       {{"", "", ""}, {"", "", ""}},
       {{"h9g_pair_kernel<8,GeoR>", "h9g_pair_kernel<8,GeoC<8,24>>", "h9g_pair_kernel<8,GeoC<8,48>>"},
        {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}},
@@ -1290,7 +1307,9 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
         "h9g_solo_kernel<10,GeoC<10,24>>+h9g_pair_kernel<10,GeoC<10,24>>",
         "h9g_solo_kernel<10,GeoC<10,48>>+h9g_pair_kernel<10,GeoC<10,48>>"}},
       {{"", "", ""},
-       {"h9g_pair2_kernel<10,GeoR>", "h9g_pair2_kernel<10,GeoC<10,24>>", "h9g_pair2_kernel<10,GeoC<10,48>>"}}};
+       {"h9g_pair2_kernel<10,GeoR>", "h9g_pair2_kernel<10,GeoC<10,24>>", "h9g_pair2_kernel<10,GeoC<10,48>>"}},
+      {{"h9g_pair11_kernel<8,GeoR>", "h9g_pair11_kernel<8,GeoC<8,24>>", "h9g_pair11_kernel<8,GeoC<8,48>>"},
+       {"h9g_pair11_kernel<10,GeoR>", "h9g_pair11_kernel<10,GeoC<10,24>>", "h9g_pair11_kernel<10,GeoC<10,48>>"}}};
   // default: the pair kernel at L = 8; at L = 10 the kernel that needs less
   // time for this many columns (l10_kind)
   if (const char *se = getenv("H9G_SORT")) ctx->sort = atoi(se) != 0;
@@ -1319,6 +1338,8 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     ctx->kind = 1;
   else if (kenv && strcmp(kenv, "pair2") == 0 && L == 10)
     ctx->kind = 4;
+  else if (kenv && strcmp(kenv, "pair11") == 0)
+    ctx->kind = 5;
   else if (kenv && strcmp(kenv, "mixed") == 0) {
     // forced split (tests): H9G_SPLIT cells on the solo kernel, else the model's
     ctx->kind = 3;
@@ -1485,14 +1506,18 @@ static int join_prefetch(h9g_ctx *ctx, int slot) {
   return rc;
 }
 
+// Cells per workgroup of a pair-kernel kind: 4 waves of 22 columns, or of 11
+// (kind 5, h9g_pair11_kernel).
+static size_t pair_block_cells(int kind) { return (size_t)(kind == 5 ? H9G_PCPW11 : H9G_PCPW) * H9G_PWAVES; }
+
 // Pacer mode of a pair launch over m cells (h9g_pair.h Pacer): pace when all
 // its workgroups are resident at once (one round), else rotate -- a wave of a
 // later round starts hundreds of days behind the waves it shares a SIMD with.
 static int pace_mode(const h9g_ctx *ctx, size_t m) {
   if (ctx->prio_mode >= 0) return ctx->prio_mode;
-  const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
+  const size_t per_block = pair_block_cells(ctx->kind);
   const size_t blocks = (m + per_block - 1) / per_block;
-  const int resident = ctx->kind == 4 ? 2 : (ctx->L <= 8 ? pair_resident<8>() : pair_resident<10>());
+  const int resident = ctx->kind == 4 ? 2 : (ctx->kind == 5 ? 3 : (ctx->L <= 8 ? pair_resident<8>() : pair_resident<10>()));
   return blocks <= (size_t)ctx->ncu * resident ? 2 : 1;
 }
 
@@ -1535,7 +1560,7 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
   const int kind = d_list ? (ctx->kind == 3 ? 1 : ctx->kind) : ctx->kind;
   const size_t ncells = d_list ? (size_t)m : ctx->n;
   if (d_list) {
-    const int pcpb = kind == 2 ? H9G_YBLOCK : H9G_PCPW * H9G_PWAVES;
+    const int pcpb = kind == 2 ? H9G_YBLOCK : (int)pair_block_cells(kind);
     if (!ctx->d_forc_s) HIPCHK(hipMalloc(&ctx->d_forc_s, sizeof(float) * 7 * (size_t)ctx->cfg.max_days * ctx->n));
     if (!ctx->d_ann_s) HIPCHK(hipMalloc(&ctx->d_ann_s, sizeof(float) * (12 + ctx->L) * ctx->n));
     a.perm = d_list;
@@ -1546,7 +1571,7 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
     a.annual = ctx->d_ann_s;
     a.sorted_io = 1;
   } else if (ctx->sort) {             // per launch range and its workgroup size (h9g_sort_kernel)
-    const int n = (int)ctx->n, ns = (int)ctx->n_solo, pcpb = H9G_PCPW * H9G_PWAVES;
+    const int n = (int)ctx->n, ns = (int)ctx->n_solo, pcpb = (int)pair_block_cells(ctx->kind);
     if (ctx->kind == 2) {
       H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, n, H9G_YBLOCK, ctx->d_st, ctx->d_err,
                    ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
@@ -1587,7 +1612,7 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
 #endif
   }
   if (kind != 2) {
-    const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
+    const size_t per_block = pair_block_cells(kind);
     const size_t need = ((ctx->n + per_block - 1) / per_block) * PairStore<8, H9G_PLANES>::GBLOCK;
     if (ctx->sv_bytes < need) {
       (void)hipFree(ctx->d_sv);
@@ -1669,6 +1694,10 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     H9G_DISPATCH_L10(ctx, h9g_pair2_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
                      ctx->sc, a);
+  } else if (kind == 5) {
+    const size_t per_block = pair_block_cells(5);
+    H9G_DISPATCH(ctx, h9g_pair11_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
+                 ctx->sc, a);
   } else {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,

@@ -81,19 +81,11 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
 #ifndef H9G_FE2
 #define H9G_FE2 1     // both, in the 2-wave build (PairStore R = 2)
 #endif
-#ifndef H9G_SPARE_PRE
-#define H9G_SPARE_PRE 1   // spare lanes' operands fetched before the rounds (hydrology_pair)
-#endif
 #ifndef H9G_SPARE_FENCE
 #define H9G_SPARE_FENCE 0      // rounds of the spare-lane phases followed by a scheduling fence (bit q)
 #endif
 #ifndef H9G_SPARE_L10
 #define H9G_SPARE_L10 0   // spare lanes in the 3-wave L = 10 build too (PairStore::kSpare)
-#endif
-#ifndef H9G_SPARE_SLOT0
-// spare lanes take the pairs' first slot instead of their last
-// (hydrology_pair; round 5: 186.5 -> 183.7 ms)
-#define H9G_SPARE_SLOT0 1
 #endif
 
 template <int K>
@@ -301,7 +293,9 @@ struct PairStore {
   // (~15 divisions per substep) instead of the day constants' reciprocals (~5;
   // round 3: 533.6 -> 530.3 ms for config 5), no 1/theta_s (72 rows).  At
   // R = 2 every reciprocal fits at L = 10 too (89 rows).
-  static constexpr bool kRecip = true, kRts = L <= 8 || R <= 2, kDayRecip = L <= 8 || R <= 2;
+  // (S = 22, the 11-column wave of h9g_pair11_kernel, leaves the LDS room for
+  // every reciprocal at L = 10 and 3 workgroups per CU too: 89 rows, 31.3 KB)
+  static constexpr bool kRecip = true, kRts = L <= 8 || R <= 2 || S <= 22, kDayRecip = L <= 8 || R <= 2 || S <= 22;
   // s_node of the conductivity phase from the stored 1/theta_s too (round 3:
   // no longer spills in the call-free kernel)
   static constexpr bool kRtsHK = kRts;
@@ -320,9 +314,10 @@ struct PairStore {
   Pacer pace;
   lds_float *wb;                       // the wave's block (column 0): spare lanes' stolen slots
   static constexpr int LANES = S;
-  // spare lanes in the per-layer phases (hydrology_pair): not in the 3-wave
-  // L = 10 build, whose registers they push further into scratch
-  static constexpr bool kSpare = H9G_SPARE_L10 || !(L >= 10 && R >= 3);
+  // helper lanes in the per-layer phases (hydrology_pair): not in the 3-wave
+  // L = 10 build of 22-column waves, whose registers they push further into
+  // scratch
+  static constexpr bool kSpare = H9G_SPARE_L10 || !(L >= 10 && R >= 3 && S >= 44);
   __device__ __forceinline__ void day_start(int day) const { pace.day_start(day, RESIDENT); }
   __device__ __forceinline__ float zi(int i) const { return zt[i]; }
   __device__ __forceinline__ float zim(int i) const { return zt[L + 2 + i]; }
@@ -1085,73 +1080,87 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
                          sel(h, theta[i0 + 1], theta[ip1]), sel(h, TS(i0 + 1), TS(ip1)), bad);
     };
     if constexpr (SP::kSpare && CS::kSpare && !M::kExact) {
-      // Spare lanes (round 4).  A wave's 22 pairs use 44 of its 64 lanes.  In
-      // these two phases -- a slot per round, NT rounds -- the 20 spare lanes
-      // evaluate the pairs' last slot (NT - 1) while the pairs do slots
-      // 0 .. NT - 2: in round q spare lane S + j takes pair lane k = j + 20q,
-      // with k's operands by ds_bpermute (all fetched before the first
-      // round) and its parameters from k's LDS column.  After the rounds pair
-      // lane k takes its result from spare lane S + k % 20 (round k / 20) and
-      // the flags of that evaluation with it.  NT - 1 rounds instead of NT,
-      // the same expressions on the same operands: no bit changes.  A flag on
-      // either side re-runs the pair lane's slots exactly, as in par_d.
-      constexpr int S = CS::LANES, NSP = 64 - S, QS = (S + NSP - 1) / NSP;   // QS: rounds with spare work
-      static_assert(QS <= NT - 1, "the spare lanes cover the last slot in NT - 1 rounds");
-      // the slot the spare lanes take (SPS) and the pairs' slot of round q.
-      // SPS = 0 (round 5): the water table lies in layers L-1 or L in most
-      // columns, and the equilibrium profile's in-layer case (a wave-uniform
-      // branch of ~20 VALU on the round's critical path, :530-543) then runs
-      // in the one round where the pairs evaluate their last slot, not in
-      // every round that holds a spare lane's last slot of another pair
-      // (branch counts: entered in 1.77 of 3 rounds with SPS = NT - 1)
-      constexpr int SPS = H9G_SPARE_SLOT0 ? 0 : NT - 1;
-      auto ps = [](int q) constexpr { return SPS == 0 ? q + 1 : q; };
+      // Helper lanes (round 4: "spare lanes"; round 5: any number of slots).
+      // A wave's C pairs use S = 2C of its 64 lanes; the other H = 64 - S
+      // lanes help in these two phases.  The phases take R = ceil(NT S / 64)
+      // rounds instead of NT: in round q every pair lane evaluates its own
+      // slot U + q (U = NT - R), and the helpers evaluate the first U slots of
+      // all pair lanes, task tau = u S + k (slot u of pair lane k) on helper
+      // S + tau % H in round tau / H, with k's operands by ds_bpermute
+      // (fetched before the rounds) and its parameters from k's LDS column.
+      // After the rounds pair lane k takes each helper result, and the flags
+      // of that evaluation, from its helper.  The same expressions on the
+      // same operands: no bit changes.  A flag on either side re-runs the
+      // pair lane's slots exactly, as in par_d.
+      //   L = 8,  C = 22: R = 3, U = 1 (round 4's spare lanes: NT - 1 rounds)
+      //   L = 10, C = 11: R = 2, U = 3 (h9g_pair11_kernel, small L = 10 shards)
+      // The helpers take the FIRST U slots (round 5): the water table lies in
+      // layers L-1 or L in most columns, and the equilibrium profile's
+      // in-layer case (a wave-uniform branch of ~20 VALU on the round's
+      // critical path, :530-543) then runs in the one round where the pairs
+      // evaluate their last slot, not in every round that holds a helper's
+      // last slot of some pair (branch counts: 1.77 of 3 rounds with the
+      // helpers on the last slot; config 2: 186.5 -> 183.7 ms).
+      constexpr int S = CS::LANES, H = 64 - S;
+      constexpr int R = (NT * S + 63) / 64, U = NT - R, TOT = U * S;
+      static_assert(U >= 1 && TOT <= R * H, "the helpers cover the first U slots in R rounds");
       const bool st = sp.spare;
       const int hh = sp.h;
-      auto kq = [&](int q) __attribute__((always_inline)) {   // spare lane: the pair lane of round q
-        const int k = sp.ln - S + NSP * (q < QS ? q : QS - 1);
-        return k < S - 1 ? k : S - 1;
+      // helper: its task in round q (idle helpers repeat the last task)
+      auto tau_q = [&](int q) __attribute__((always_inline)) {
+        const int t = q * H + (st ? sp.ln - S : 0);
+        return t < TOT ? t : TOT - 1;
       };
-      const int qo = sp.ln / NSP, src = S + sp.ln % NSP;   // pair lane: round and spare lane of its last slot
-      // operands fetched before the rounds (latency off the rounds' path), or
-      // in each round (fewer live registers).  A ds_bpermute must run in
-      // converged control flow: a lane reads only what active lanes provide
-      // (a spare-lanes-only fetch under `st ?` read zeros: wrong results).
-      constexpr bool kPre = H9G_SPARE_PRE;
-      auto back = [&](const float (&v)[NT - 1]) __attribute__((always_inline)) {
-        float x = lane_get(v[0], src);
+      // pair lane: the helper lane of its slot u, and the round it ran in
+      auto src_u = [&](int u) __attribute__((always_inline)) { return S + (u * S + sp.ln) % H; };
+      auto qo_u = [&](int u) __attribute__((always_inline)) { return (u * S + sp.ln) / H; };
+      // rounds that hold tasks of slot u, and slots that round q holds
+      auto qlo = [](int u) constexpr { return (u * S) / H; };
+      auto qhi = [](int u) constexpr { return ((u * S + S - 1) / H) < R - 1 ? (u * S + S - 1) / H : R - 1; };
+      auto ulo = [](int q) constexpr { return (q * H) / S < U - 1 ? (q * H) / S : U - 1; };
+      auto uhi = [](int q) constexpr { return (q * H + H - 1) / S < U - 1 ? (q * H + H - 1) / S : U - 1; };
+      // a helper result of every round -> pair lane's slot u.  A ds_bpermute
+      // must run in converged control flow: a lane reads only what active
+      // lanes provide (a helpers-only fetch under `st ?` read zeros).
+      auto back = [&](const float (&v)[R], int u) __attribute__((always_inline)) {
+        const int src = src_u(u), qo = qo_u(u);
+        float x = lane_get(v[qlo(u)], src);
 #pragma unroll
-        for (int q = 1; q < QS; q++) {
+        for (int q = qlo(u) + 1; q <= qhi(u); q++) {
           const float g = lane_get(v[q], src);
           x = qo == q ? g : x;
         }
         return x;
       };
-      {
-        float zwk[QS];
-        if constexpr (kPre) {
+      auto flags_back = [&](int fl) __attribute__((always_inline)) {
+        bool any = false;
 #pragma unroll
-          for (int q = 0; q < QS; q++) zwk[q] = lane_get(zwtmm, kq(q));
-        }
+        for (int u = 0; u < U; u++) any |= ((lane_geti(fl, src_u(u)) >> qo_u(u)) & 1) != 0;
+        return any;
+      };
+      {
+        float zwk[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) zwk[q] = lane_get(zwtmm, tau_q(q) % S);
         FV<1> r[NT];
-        float rv[NT - 1];
+        float rv[R];
         int fl = 0;
 #pragma unroll
-        for (int q = 0; q < NT - 1; q++) {
-          const int k = kq(q);
-          const lds_float *o = st ? cs.wb + k + SPS * S : cs.self + ps(q) * S;
-          const float zwq = kPre ? zwk[q < QS ? q : QS - 1] : lane_get(zwtmm, k);   // in every lane (below)
+        for (int q = 0; q < R; q++) {
+          const int tau = tau_q(q), k = tau % S, u = tau / S;
+          const int t = U + q;
+          const lds_float *o = st ? cs.wb + k + u * S : cs.self + t * S;
           bool b = false;
-          r[ps(q)] = eq_body(st ? 2 * SPS + 1 + (k & 1) : 2 * ps(q) + 1 + hh,
-                             [&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
-                             st ? zwq : zwtmm, b);
-          rv[q] = r[ps(q)].v[0];
+          r[t] = eq_body(st ? 2 * u + 1 + (k & 1) : 2 * t + 1 + hh,
+                         [&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
+                         st ? zwk[q] : zwtmm, b);
+          rv[q] = r[t].v[0];
           fl |= (b ? 1 : 0) << q;
           if ((H9G_SPARE_FENCE >> q) & 1) sched_fence();
         }
-        r[SPS].v[0] = back(rv);
-        const int gf = lane_geti(fl, src);
-        const bool bad = !st & ((fl | ((gf >> qo) & 1)) != 0);
+#pragma unroll
+        for (int u = 0; u < U; u++) r[u].v[0] = back(rv, u);
+        const bool bad = !st & ((fl != 0) | flags_back(fl));
         if (__builtin_expect(bad, 0)) {
 #pragma unroll
           for (int t = 0; t < NT; t++) r[t] = eq_exact(t, hh);
@@ -1161,49 +1170,57 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
       }
       pr.mark(2);
       {
-        // this lane's operands of slot SPS (theta(i), theta(ip), ip = min(i + 1, L))
-        const float th_l = sel(hh, theta[2 * SPS + 1], theta[2 * SPS + 2]);
-        const float thp_l = sel(hh, theta[2 * SPS + 2], theta[2 * SPS + 3 <= L ? 2 * SPS + 3 : L]);
-        float thk[QS], thpk[QS];
-        if constexpr (kPre) {
+        // this lane's operands of its helper slots u (theta(i), theta(ip),
+        // ip = i + 1 <= L as u <= NT - 2), and each helper's of its tasks
+        float thu[U], thpu[U];
 #pragma unroll
-          for (int q = 0; q < QS; q++) {
-            thk[q] = lane_get(th_l, kq(q));
-            thpk[q] = lane_get(thp_l, kq(q));
+        for (int u = 0; u < U; u++) {
+          thu[u] = sel(hh, theta[2 * u + 1], theta[2 * u + 2]);
+          thpu[u] = sel(hh, theta[2 * u + 2], theta[2 * u + 3]);
+        }
+        float thk[R], thpk[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+          const int tau = tau_q(q), k = tau % S, u = tau / S;
+          float a = lane_get(thu[ulo(q)], k), b = lane_get(thpu[ulo(q)], k);
+#pragma unroll
+          for (int w = ulo(q) + 1; w <= uhi(q); w++) {
+            const float ga = lane_get(thu[w], k), gb = lane_get(thpu[w], k);
+            a = u == w ? ga : a;
+            b = u == w ? gb : b;
           }
+          thk[q] = a;
+          thpk[q] = b;
         }
         const lds_float *pe = cs.even + PF_TS * NT * S + (hh ? S : 1);           // TS(i + 1), TS(ip) of own slots
         FV<4> r[NT];
+        float rv[4][R];
         int fl = 0;
 #pragma unroll
-        for (int q = 0; q < NT - 1; q++) {
-          const int k = kq(q), qq = q < QS ? q : QS - 1;
-          const int t = ps(q);
-          const lds_float *o = st ? cs.wb + k + SPS * S : cs.self + t * S;
+        for (int q = 0; q < R; q++) {
+          const int tau = tau_q(q), k = tau % S, u = tau / S;
+          const int t = U + q;
+          const lds_float *o = st ? cs.wb + k + u * S : cs.self + t * S;
           // TS(ip) of the slot: layer 2t+2 (odd column, row t) for the even
           // lane, 2t+3 (even column, row t+1) for the odd one; TS(L) (odd
           // column, row NT-1) in the last slot
-          const lds_float *pt_sp = SPS == NT - 1 ? cs.wb + (k | 1) + (PF_TS * NT + NT - 1) * S
-                                                 : cs.wb + ((k & 1) ? (k & ~1) + S : (k | 1)) + (PF_TS * NT + SPS) * S;
+          const lds_float *pt_h = cs.wb + ((k & 1) ? (k & ~1) + S : (k | 1)) + (PF_TS * NT + u) * S;
           const lds_float *pt_own = t == NT - 1 ? cs.even + 1 + (PF_TS * NT + NT - 1) * S : pe + t * S;
-          const lds_float *pt = st ? pt_sp : pt_own;
-          const float thq = kPre ? thk[qq] : lane_get(th_l, k), thpq = kPre ? thpk[qq] : lane_get(thp_l, k);
+          const lds_float *pt = st ? pt_h : pt_own;
           bool b = false;
           r[t] = hk_body([&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
-                         st ? thq : sel(hh, theta[2 * t + 1], theta[2 * t + 2]),
-                         st ? thpq : sel(hh, theta[2 * t + 2], theta[2 * t + 3 <= L ? 2 * t + 3 : L]), *pt, b);
+                         st ? thk[q] : sel(hh, theta[2 * t + 1], theta[2 * t + 2]),
+                         st ? thpk[q] : sel(hh, theta[2 * t + 2], theta[2 * t + 3 <= L ? 2 * t + 3 : L]), *pt, b);
+#pragma unroll
+          for (int kk = 0; kk < 4; kk++) rv[kk][q] = r[t].v[kk];
           fl |= (b ? 1 : 0) << q;
           if ((H9G_SPARE_FENCE >> q) & 1) sched_fence();
         }
 #pragma unroll
-        for (int kk = 0; kk < 4; kk++) {
-          float rv[NT - 1];
+        for (int kk = 0; kk < 4; kk++)
 #pragma unroll
-          for (int q = 0; q < NT - 1; q++) rv[q] = r[ps(q)].v[kk];
-          r[SPS].v[kk] = back(rv);
-        }
-        const int gf = lane_geti(fl, src);
-        const bool bad = !st & ((fl | ((gf >> qo) & 1)) != 0);
+          for (int u = 0; u < U; u++) r[u].v[kk] = back(rv[kk], u);
+        const bool bad = !st & ((fl != 0) | flags_back(fl));
         if (__builtin_expect(bad, 0)) {
 #pragma unroll
           for (int t = 0; t < NT; t++) r[t] = hk_exact(t, hh);

@@ -23,11 +23,12 @@ def _gpu_run(inp, L):
                  grow_on=bool(inp["grow_on"]), state0=inp["state0"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "solo", "mixed"])
+@pytest.mark.parametrize("kernel", ["pair", "pair11", "solo", "mixed"])
 @pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit", "spinup")))
 def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
-    """Both year kernels (two lanes per column = the default; one lane), and
-    both in one run (cells [0, 37) on the solo kernel, the rest on pair)."""
+    """The year kernels (two lanes per column = the default, with 22 or 11
+    columns per wave; one lane), and two in one run (cells [0, 37) on the
+    solo kernel, the rest on pair)."""
     monkeypatch.setenv("H9G_KERNEL", kernel)
     monkeypatch.setenv("H9G_SPLIT", "37")
     meta, inp, exp = load_golden(name)
@@ -37,7 +38,7 @@ def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
     assert same_bits(out["state"], exp["state"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "solo"])
+@pytest.mark.parametrize("kernel", ["pair", "pair11", "solo"])
 @pytest.mark.parametrize("name", golden_names(kind=("stop",)))
 def test_gpu_reproduces_reference_stop(name, kernel, monkeypatch):
     monkeypatch.setenv("H9G_KERNEL", kernel)
@@ -71,7 +72,7 @@ def test_config4_spinup_decades_carry_state():
     assert same_bits(d2["state"], exp["state"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "pair2", "solo", "mixed"])
+@pytest.mark.parametrize("kernel", ["pair", "pair2", "pair11", "solo", "mixed"])
 def test_config5_l10_matches_reference_golden(kernel, monkeypatch):
     """Config 5 (0.25 deg, L = 10, NS = 24, GROW) against the reference
     rebuilt with nsoil_layers_max = 10: every annual mean (NaN for the cell
@@ -119,7 +120,7 @@ def test_gpu_reproduces_bench_stop(kernel, monkeypatch):
     assert same_bits(refcase.pack_state(st, meta["L"]), exp["state_ok"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "solo"])
+@pytest.mark.parametrize("kernel", ["pair", "pair11", "solo"])
 def test_gpu_nan_parameter_cells_match_oracle(kernel, monkeypatch):
     """Cells with missing soil data (NaN Fmax, a NaN layer parameter) run
     the year with NaN state, so every deferred special-case check of the
@@ -226,7 +227,7 @@ def test_config4_full_grid_30_years_sampled_against_oracle():
         assert same_bits(got[k][sample], v), k
 
 
-@pytest.mark.parametrize("kernel", ["pair", "pair2", "solo", "mixed"])
+@pytest.mark.parametrize("kernel", ["pair", "pair2", "pair11", "solo", "mixed"])
 def test_config5_l10_quarter_degree_sample(kernel, monkeypatch):
     """10 soil layers (config 5) on 0.25 deg cells, NS=24, GROW on, the
     year kernels (pair at 3 and at 2 waves per SIMD, solo) and the mixed
@@ -273,13 +274,14 @@ def test_shard_invariance_and_determinism():
     assert same_bits(np.concatenate(parts, axis=2), ann_full)
 
 
-@pytest.mark.parametrize("L,nisurf,kernel", [(8, 48, "pair"), (10, 24, "pair2")])
+@pytest.mark.parametrize("L,nisurf,kernel", [(8, 48, "pair"), (10, 24, "pair2"), (8, 48, "pair11"),
+                                             (10, 24, "pair11")])
 def test_spare_lanes_in_ragged_waves(L, nisurf, kernel, monkeypatch):
-    """The 20 spare lanes of a pair-kernel wave evaluate the pairs' last layer
-    slot and mirror pair lane j mod (the wave's pair lanes) elsewhere
-    (h9g.hip pair_body).  Waves with 1, 3, 9 and 22 + 1 columns (the mirror
-    wraps; a second, one-column wave) give the same bits for every cell as
-    the same cells inside a 1,500-cell run of full waves."""
+    """The helper lanes of a pair-kernel wave (20 with 22 columns, 42 with
+    11) evaluate the pairs' first layer slots and mirror a pair lane
+    elsewhere (h9g.hip pair_body).  Waves with 1, 3, 9 and 22 + 1 columns
+    (the mirror wraps; a second, one-column wave) give the same bits for
+    every cell as the same cells inside a 1,500-cell run of full waves."""
     monkeypatch.setenv("H9G_KERNEL", kernel)
     gid = synth.land_cells()[::31][:1500]
     ann_all, st_all, _ = _full_grid_gpu(gid, L, nisurf, True, 1901, 2)

@@ -26,7 +26,7 @@ def main():
         sl = shard_slice(gid.size, 0, world)
         g, la = gid[sl], lat[sl]
         row = [f"N={world} cells={g.size}"]
-        for k in os.environ.get("L10_KINDS", "pair,pair2,solo,mixed,auto").split(","):
+        for k in os.environ.get("L10_KINDS", "pair,pair2,pair11,solo,mixed,auto").split(","):
             if k == "auto":
                 os.environ.pop("H9G_KERNEL", None)
             else:
