@@ -284,6 +284,18 @@ h9g_pair11_kernel(const KArgs a, const G g) {
   pair_body<L, G, 3, H9G_PCPW11>(a, g);
 }
 
+// One column per wave (round 5): the 62 lanes past the pair help in the
+// per-layer phases, which take one round each (hydrology_pair helpers), and
+// the wave may hold every register (one wave per SIMD: no spills).  For the
+// short lists of the cell-order re-runs (h9g_run_decade_ordered), whose
+// years run as lone waves: a lone wave's year is latency-bound, and this
+// cuts its per-layer rounds from 3 to 1 at L = 8 (from 5 to 1 at L = 10).
+template <int L, class G>
+__global__ void __launch_bounds__(64 * H9G_PWAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
+h9g_pair1_kernel(const KArgs a, const G g) {
+  pair_body<L, G, 1, 1>(a, g);
+}
+
 
 // Solo kernel: one lane per soil column running the generic code of
 // h9g_pair.h with one lane doing every layer (SplitAll: two layers per
@@ -1098,6 +1110,7 @@ template __global__ void h9g_pair_kernel<10, GeoC<10, 24>>(const KArgs, const Ge
 template __global__ void h9g_pair2_kernel<10, GeoC<10, 24>>(const KArgs, const GeoC<10, 24>);
 template __global__ void h9g_pair11_kernel<10, GeoC<10, 24>>(const KArgs, const GeoC<10, 24>);
 #else
+template __global__ void h9g_pair1_kernel<8, GeoC<8, 48>>(const KArgs, const GeoC<8, 48>);
 template __global__ void h9g_pair_kernel<8, GeoC<8, 48>>(const KArgs, const GeoC<8, 48>);
 #endif
 #else
@@ -1508,7 +1521,12 @@ static int join_prefetch(h9g_ctx *ctx, int slot) {
 
 // Cells per workgroup of a pair-kernel kind: 4 waves of 22 columns, or of 11
 // (kind 5, h9g_pair11_kernel).
-static size_t pair_block_cells(int kind) { return (size_t)(kind == 5 ? H9G_PCPW11 : H9G_PCPW) * H9G_PWAVES; }
+static size_t pair_block_cells(int kind) {
+  return (size_t)(kind == 5 ? H9G_PCPW11 : (kind == 6 ? 1 : H9G_PCPW)) * H9G_PWAVES;
+}
+// Lists of at most this many cells (the cell-order re-runs' tails) run on
+// h9g_pair1_kernel: every workgroup resident at one wave per SIMD.
+#define H9G_PAIR1_MAX 1024
 
 // Pacer mode of a pair launch over m cells (h9g_pair.h Pacer): pace when all
 // its workgroups are resident at once (one round), else rotate -- a wave of a
@@ -1557,7 +1575,10 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
   a.hist = ctx->d_hist;
   // the launch's kernel: a list runs on the pair kernel (or the one the
   // context's shard size chose at L = 10), never split into solo rounds
-  const int kind = d_list ? (ctx->kind == 3 ? 1 : ctx->kind) : ctx->kind;
+  // short lists (the cell-order re-runs' tails) on the one-column kernel
+  const int kind = d_list ? (m <= H9G_PAIR1_MAX && ctx->kind != 2 && !getenv("H9G_NO_PAIR1") ? 6
+                                                                               : (ctx->kind == 3 ? 1 : ctx->kind))
+                          : ctx->kind;
   const size_t ncells = d_list ? (size_t)m : ctx->n;
   if (d_list) {
     const int pcpb = kind == 2 ? H9G_YBLOCK : (int)pair_block_cells(kind);
@@ -1697,6 +1718,10 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
   } else if (kind == 5) {
     const size_t per_block = pair_block_cells(5);
     H9G_DISPATCH(ctx, h9g_pair11_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
+                 ctx->sc, a);
+  } else if (kind == 6) {
+    const size_t per_block = pair_block_cells(6);
+    H9G_DISPATCH(ctx, h9g_pair1_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
                  ctx->sc, a);
   } else {
     const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;

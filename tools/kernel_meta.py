@@ -70,7 +70,7 @@ def main() -> None:
     print(f"{'kernel':60s} {'VGPR':>5s} {'AGPR':>5s} {'SGPR':>5s} {'VGPR spill':>10s} {'SGPR spill':>10s} "
           f"{'private B':>9s} {'LDS B':>7s}")
     for k, nm in sorted(zip(ks, names), key=lambda x: x[1]):
-        if "--all" not in sys.argv and not re.search(r"h9g_(pair|pair2|pair11|solo)_kernel", nm):
+        if "--all" not in sys.argv and not re.search(r"h9g_(pair|pair1|pair2|pair11|solo)_kernel", nm):
             continue
         short = nm.replace("h9k::", "").replace("(KArgs, ", "(")
         print(f"{short[:60]:60s} {k.get('vgpr', 0):5d} {k.get('agpr', 0):5d} {k.get('sgpr', 0):5d} "
