@@ -84,6 +84,9 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
 #ifndef H9G_SPARE_FENCE
 #define H9G_SPARE_FENCE 0      // rounds of the spare-lane phases followed by a scheduling fence (bit q)
 #endif
+#ifndef H9G_INL_LAST
+#define H9G_INL_LAST 0   // the in-layer case branch-free in the pairs' last-slot round (hydrology_pair)
+#endif
 #ifndef H9G_SPARE_L10
 #define H9G_SPARE_L10 0   // spare lanes in the 3-wave L = 10 build too (PairStore::kSpare)
 #endif
@@ -959,7 +962,9 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
     // the slot of layer il, with O(p) the slot's value of field p and zw the
     // water table (mm): a lane's own slot (eq_fast) or, on a spare lane,
     // another pair's last slot (below).
-    auto eq_body = [&](int il, auto O, float zw, bool &bad) __attribute__((always_inline)) -> FV<1> {
+    // inl_all: evaluate the in-layer case for every lane, branch-free (the
+    // round where the pairs evaluate their last slot, H9G_INL_LAST)
+    auto eq_body = [&](int il, auto O, float zw, bool &bad, bool inl_all) __attribute__((always_inline)) -> FV<1> {
           const float zlo = cs.zi(il - 1), zhi = cs.zi(il);
           const float ts = O(PF_TS), psi = O(PF_PSI);
           const bool sat = zw <= zlo;
@@ -979,7 +984,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           // column, so evaluated only in a slot where some lane of the wave
           // has it (a wave-uniform branch)
           float vin = zero;
-          if (any_lane(inl)) {
+          if (inl_all || any_lane(inl)) {
           H9G_BR(BR_INL);
           const float d0 = zw - zlo;
           const float q1 = m.div_d(O(PF_PTE), d0, recip64(d0));
@@ -1001,7 +1006,8 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           return FV<1>{{MAXC(smpmin, z)}};
     };
     auto eq_fast = [&](int t, int h, bool &bad) __attribute__((always_inline)) -> FV<1> {
-          return eq_body(2 * t + 1 + h, [&](int p) __attribute__((always_inline)) { return OWN(p); }, zwtmm, bad);
+          return eq_body(2 * t + 1 + h, [&](int p) __attribute__((always_inline)) { return OWN(p); }, zwtmm, bad,
+                         false);
     };
     auto hk_exact = [&](int t, int h) __attribute__((always_inline)) -> FV<4> {
           H9G_BR(BR_HKX);
@@ -1153,7 +1159,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           bool b = false;
           r[t] = eq_body(st ? 2 * u + 1 + (k & 1) : 2 * t + 1 + hh,
                          [&](int p) __attribute__((always_inline)) { return o[p * NT * S]; },
-                         st ? zwk[q] : zwtmm, b);
+                         st ? zwk[q] : zwtmm, b, H9G_INL_LAST && U + q == NT - 1);
           rv[q] = r[t].v[0];
           fl |= (b ? 1 : 0) << q;
           if ((H9G_SPARE_FENCE >> q) & 1) sched_fence();
