@@ -2088,7 +2088,7 @@ int h9g_sync(h9g_ctx *ctx) {
     static const char *names[BR_N] = {"substep", "theta", "qb", "eq_exact", "aqpow", "aq_s", "hk_exact", "tri_flux",
                                       "tri_sweep", "recharge", "baseflow", "watmin", "rerun", "powf_redo",
                                       "div_redo", "expf_redo", "powf_fix", "div_fix", "inl", "any_aq", "jwt_col",
-                                      "visit2", "snap", "day"};
+                                      "visit2", "snap", "eb_exact", "day"};
     unsigned long long c[64];
     HIPCHK(hipMemcpyFromSymbol(c, HIP_SYMBOL(h9g_branch_count), sizeof(c)));
     const double ws = c[BR_SUBSTEP] ? (double)c[BR_SUBSTEP] : 1.0;

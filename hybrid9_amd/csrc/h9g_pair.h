@@ -85,7 +85,15 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
 #define H9G_SPARE_FENCE 0      // rounds of the spare-lane phases followed by a scheduling fence (bit q)
 #endif
 #ifndef H9G_INL_LAST
-#define H9G_INL_LAST 0   // the in-layer case branch-free in the pairs' last-slot round (hydrology_pair)
+// the in-layer case branch-free in the pairs' last-slot round (hydrology_pair;
+// round 5: 182.7 -> 181.8 ms, three alternating pairs on one box)
+#define H9G_INL_LAST 1
+#endif
+#ifndef H9G_EB_FAST
+#define H9G_EB_FAST 1    // round 5: 182.2 -> 181.7 ms; the energy balance's quotients branch-free, runtime divisors by Markstein (hydrology_pair)
+#endif
+#ifndef H9G_AQ_FREE
+#define H9G_AQ_FREE 0    // the aquifer node's second round and interface branch-free (hydrology_pair)
 #endif
 #ifndef H9G_SPARE_L10
 #define H9G_SPARE_L10 0   // spare lanes in the 3-wave L = 10 build too (PairStore::kSpare)
@@ -822,24 +830,104 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
 #pragma unroll
     for (int i = 1; i <= L; i++) beta = beta + rb[i];
   }
-  // :283-295
-  float rsc;
-  if ((DC(D_OK) != zero) && (beta > zero))
-    rsc = DC(D_X) / (DC(D_LAI2) * beta * DC(D_PW28));
-  else
-    rsc = 1.0E6f;
-  rsc = MAXF(rsc, DC(D_RSCMIN));
   // :325-331
   float rss;
   if (theta[1] <= 0.15f)
     rss = (10.0f + DC(D_LIT1000)) * m.expf(0.3563f * 100.0f * (0.15f - theta[1]));
   else
     rss = (10.0f + DC(D_LIT1000) * (1.0f - divr<CS::kRts>(m, theta[1], TS(1), [&]() { return lay_d(cs, PF_RTS0, 1); })));
+  const float desatdT = DC(D_DESAT), gamma = DC(D_GAMMA);
+  const float Ra = DC(D_DG) * DC(D_RAA);
+  float rsc, tran, evg;
+  bool eb_fast = false;
+  if constexpr (H9G_EB_FAST && !M::kExact && CS::kDayRecip) {
+    // The energy balance's chain of quotients (:283-389) branch-free: the
+    // day constants' by their stored double reciprocals (MathFast::div_d),
+    // the runtime divisors by Markstein's correction of the refined
+    // v_rcp_f32 reciprocal, RN(x y), y = fma(fma(-d, r, 1), r, r): exact for
+    // every pair of float significands (tools/markstein_exhaustive.hip mode
+    // 1) whenever |x| and |d| lie in [2^-60, 2^60) (x = 0 included in the
+    // flagged case).  Six dependent operations instead of the IEEE
+    // division's nine.  Any flag on any lane of the wave re-runs the block
+    // below exactly (wave-uniform: the pair exchanges values).
+    bool bad = false;
+    auto mdiv = [&](float x, float d) __attribute__((always_inline)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      const float r = __builtin_amdgcn_rcpf(d);
+#else
+      const float r = 1.0f / d;
+#endif
+      const float y = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
+      const float q0 = x * y;
+      const float q = __builtin_fmaf(__builtin_fmaf(-d, q0, x), y, q0);
+      const uint32_t ux = (__builtin_bit_cast(uint32_t, x) & 0x7fffffffu) - 0x21800000u;   // 2^-60
+      const uint32_t ud = (__builtin_bit_cast(uint32_t, d) & 0x7fffffffu) - 0x21800000u;
+      bad |= (ux > ud ? ux : ud) >= 0x5d800000u - 0x21800000u;                             // 2^60
+      return q;
+    };
+    auto ddiv = [&](float x, double r) __attribute__((always_inline)) {
+      const float q = m.div_d(x, zero, r);
+      bad |= m.div_bad(q);
+      return q;
+    };
+    // :283-295
+    const bool open = (DC(D_OK) != zero) && (beta > zero);
+    bool bo = bad;
+    const float q_rsc = mdiv(DC(D_X), DC(D_LAI2) * beta * DC(D_PW28));
+    bad = bo | (open && bad);
+    float rscf = open ? q_rsc : 1.0E6f;
+    rscf = MAXF(rscf, DC(D_RSCMIN));
+    // :344-389
+    FV<2> c2, s2;
+    sp.template pick<2>(
+        [&](int h) __attribute__((always_inline)) -> FV<2> {
+          const float r = sel(h, rscf, rss);
+          const float q = ddiv(r, sp.own_day_rp(cs, DRP_RAARA, h));
+          const float PM = mdiv(sp.own_sc(cs, PS_DAY + D_NUMC, h), desatdT + gamma * (one + q));
+          const float R = sp.own_sc(cs, PS_DAY + D_DGRAC, h) + gamma * r;
+          return FV<2>{{PM, R}};
+        },
+        c2, s2);
+    FV<1> cc, cs1;
+    sp.template pick<1>(
+        [&](int h) __attribute__((always_inline)) -> FV<1> {
+          const float Rh = sel(h, c2.v[1], s2.v[1]), Ro = sel(h, s2.v[1], c2.v[1]);
+          return FV<1>{{mdiv(one, one + mdiv(Rh * Ra, Ro * (Rh + Ra)))}};
+        },
+        cc, cs1);
+    const float LEf = cc.v[0] * c2.v[0] + cs1.v[0] * s2.v[0];
+    const float VDD0f = DC(D_VDD) + ddiv((DC(D_A1) - DC(D_DG) * LEf) * DC(D_RAA), cs.day_r(DR_RHOCP));
+    FV<1> ft, fe;
+    sp.template pick<1>(
+        [&](int h) __attribute__((always_inline)) -> FV<1> {
+          const float r = sel(h, rscf, rss);
+          const double rr = sp.own_day_rp(cs, DRP_RA, h);
+          const float LEh = mdiv(sp.own_sc(cs, PS_DAY + D_DRR, h) + ddiv(DC(D_RHOCP) * VDD0f, rr),
+                                 desatdT + gamma * (1.0f + ddiv(r, rr)));
+          return FV<1>{{ddiv(LEh * 1.0E3f, cs.day_r(DR_RL))}};
+        },
+        ft, fe);
+#if defined(H9G_FORCE_RERUN)   // test builds: the exact block in about one wave-substep of two
+    bad |= (__builtin_bit_cast(uint32_t, theta[1]) & 15u) == 0;
+#endif
+    if (!__builtin_expect(any_lane(bad), 0)) {
+      rsc = rscf;
+      tran = ft.v[0];
+      evg = fe.v[0];
+      eb_fast = true;
+    }
+  }
+  if (!eb_fast) {
+  H9G_BR(BR_EBX);
+  // :283-295
+  if ((DC(D_OK) != zero) && (beta > zero))
+    rsc = DC(D_X) / (DC(D_LAI2) * beta * DC(D_PW28));
+  else
+    rsc = 1.0E6f;
+  rsc = MAXF(rsc, DC(D_RSCMIN));
   // :344-389.  The canopy (h = 0) and soil (h = 1) halves have the same
   // expressions on different operands: each lane of a pair evaluates one
   // (pick), reading its operands from its own column (D_NUMC comment).
-  const float desatdT = DC(D_DESAT), gamma = DC(D_GAMMA);
-  const float Ra = DC(D_DG) * DC(D_RAA);
   FV<2> ebc, ebs;                                       // {PM, R}: canopy, soil
   sp.template pick<2>(
       [&](int h) __attribute__((always_inline)) -> FV<2> {
@@ -873,8 +961,9 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
         return FV<1>{{divr<CS::kDayRecip>(m, LEh * 1.0E3f, DC(D_RL), [&]() { return cs.day_r(DR_RL); })}};
       },
       ftr, fev);
-  const float tran = ftr.v[0];
-  float evg = fev.v[0];
+  tran = ftr.v[0];
+  evg = fev.v[0];
+  }
   // :396-400
   float em1 = m.div(g.dz(1) * (theta[1] - watmin), dt, g.rdt()) - tran * ROOT(1);
   em1 = MAXF(zero, em1);
@@ -1260,7 +1349,9 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
   // aquifer row, :581-590, :737-741) is read only by lanes below the column:
   // a wave with none skips it (wave-uniform); the deepening loop's rare
   // fall-through below the column evaluates s_y(L) itself for a lane inside.
-  const bool any_aq = any_lane(aq);
+  // (H9G_AQ_FREE: evaluated by every wave; lanes inside the column take
+  // operands that make it an identity and raise no flag)
+  const bool any_aq = H9G_AQ_FREE || any_lane(aq);
   const int jc = aq ? L : jwt + 1;            // the layer whose -psi divides
   float s1c = one, bsw_c = zero;              // recharge operands of layer jwt+1 (:866-873)
   if (any_lane(!aq)) {

@@ -152,7 +152,7 @@ __device__ const float *h9g_aq_base;   // the annual array: cell = acc - base
 enum : int {   // H9G_BR sites
   BR_SUBSTEP = 0, BR_THETA, BR_QB, BR_EQX, BR_AQPOW, BR_AQS, BR_HKX, BR_TRIFLUX, BR_TRISWEEP, BR_RECH,
   BR_BASE, BR_WATMIN, BR_RERUN, BR_POWREDO, BR_DIVREDO, BR_EXPREDO, BR_POWFIX, BR_DIVFIX, BR_INL, BR_ANYAQ,
-  BR_JWTCOL, BR_VISIT2, BR_SNAP, BR_DAY, BR_N
+  BR_JWTCOL, BR_VISIT2, BR_SNAP, BR_EBX, BR_DAY, BR_N
 };
 
 // ------------------------------------------------------------ math policies

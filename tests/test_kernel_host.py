@@ -160,3 +160,16 @@ def test_rerun_without_day_snapshot_is_reported():
     err = out["err"]
     assert (err[:, 0] == 5).all() and (err[:, 1] == 0).all()
     assert (err[:, 2] == 0).all() and (err[:, 3] == 4).all()
+
+
+@pytest.mark.parametrize("name", ["c1_2yr_leap", "c4_spinup"])
+def test_exact_energy_balance_build(name):
+    """The energy balance's exact block (h9g_pair.h, run when the branch-free
+    block flags a quotient outside the Markstein range) as the whole path:
+    a -DH9G_EB_FAST=0 build must give the reference's bits too."""
+    so = C.CDLL(str(_build_lib(["-DH9G_EB_FAST=0"])))
+    so.h9k_host_run.argtypes = lib().h9k_host_run.argtypes
+    meta, inp, exp = load_golden(name)
+    out = host_run(const_geo=1, so=so, **inp)
+    assert out["rc"] == 0
+    assert same_bits(out["annual"], exp["annual"]) and same_bits(out["state"], exp["state"])
