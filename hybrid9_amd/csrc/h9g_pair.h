@@ -92,6 +92,12 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
 #ifndef H9G_EB_FAST
 #define H9G_EB_FAST 1    // round 5: 182.2 -> 181.7 ms; the energy balance's quotients branch-free, runtime divisors by Markstein (hydrology_pair)
 #endif
+#ifndef H9G_HK_MDIV
+#define H9G_HK_MDIV 1    // the conductivity phase's dsmpdw quotient by Markstein at L = 8 (hk_body; round 5: -0.3%; L = 10: +0.8%)
+#endif
+#ifndef H9G_INL_MDIV
+#define H9G_INL_MDIV 0   // the in-layer case's PTE / (zw - zlo) by Markstein (eq_body) instead of recip64
+#endif
 #ifndef H9G_AQ_FREE
 #define H9G_AQ_FREE 0    // the aquifer node's second round and interface branch-free (hydrology_pair)
 #endif
@@ -840,35 +846,23 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
   const float Ra = DC(D_DG) * DC(D_RAA);
   float rsc, tran, evg;
   bool eb_fast = false;
-  if constexpr (H9G_EB_FAST && !M::kExact && CS::kDayRecip) {
+  if constexpr (H9G_EB_FAST && !M::kExact && (CS::kDayRecip || H9G_EB_FAST >= 2)) {
     // The energy balance's chain of quotients (:283-389) branch-free: the
     // day constants' by their stored double reciprocals (MathFast::div_d),
-    // the runtime divisors by Markstein's correction of the refined
-    // v_rcp_f32 reciprocal, RN(x y), y = fma(fma(-d, r, 1), r, r): exact for
-    // every pair of float significands (tools/markstein_exhaustive.hip mode
-    // 1) whenever |x| and |d| lie in [2^-60, 2^60) (x = 0 included in the
-    // flagged case).  Six dependent operations instead of the IEEE
-    // division's nine.  Any flag on any lane of the wave re-runs the block
-    // below exactly (wave-uniform: the pair exchanges values).
+    // the runtime divisors by mk_div (Markstein's correction of the refined
+    // v_rcp_f32 reciprocal, range-flagged).  Any flag on any lane of the
+    // wave re-runs the block below exactly (wave-uniform: the pair exchanges
+    // values).
     bool bad = false;
-    auto mdiv = [&](float x, float d) __attribute__((always_inline)) {
-#if defined(__HIP_DEVICE_COMPILE__)
-      const float r = __builtin_amdgcn_rcpf(d);
-#else
-      const float r = 1.0f / d;
-#endif
-      const float y = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
-      const float q0 = x * y;
-      const float q = __builtin_fmaf(__builtin_fmaf(-d, q0, x), y, q0);
-      const uint32_t ux = (__builtin_bit_cast(uint32_t, x) & 0x7fffffffu) - 0x21800000u;   // 2^-60
-      const uint32_t ud = (__builtin_bit_cast(uint32_t, d) & 0x7fffffffu) - 0x21800000u;
-      bad |= (ux > ud ? ux : ud) >= 0x5d800000u - 0x21800000u;                             // 2^60
-      return q;
-    };
-    auto ddiv = [&](float x, double r) __attribute__((always_inline)) {
-      const float q = m.div_d(x, zero, r);
-      bad |= m.div_bad(q);
-      return q;
+    auto mdiv = [&](float x, float d) __attribute__((always_inline)) { return mk_div(x, d, bad); };
+    auto ddiv = [&](float x, float d, auto rget) __attribute__((always_inline)) {
+      if constexpr (CS::kDayRecip) {   // the store has the day constants' double reciprocals
+        const float q = m.div_d(x, d, rget());
+        bad |= m.div_bad(q);
+        return q;
+      } else {
+        return mdiv(x, d);
+      }
     };
     // :283-295
     const bool open = (DC(D_OK) != zero) && (beta > zero);
@@ -882,7 +876,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
     sp.template pick<2>(
         [&](int h) __attribute__((always_inline)) -> FV<2> {
           const float r = sel(h, rscf, rss);
-          const float q = ddiv(r, sp.own_day_rp(cs, DRP_RAARA, h));
+          const float q = ddiv(r, sp.own_sc(cs, PS_DAY + D_RAARAC, h), [&]() { return sp.own_day_rp(cs, DRP_RAARA, h); });
           const float PM = mdiv(sp.own_sc(cs, PS_DAY + D_NUMC, h), desatdT + gamma * (one + q));
           const float R = sp.own_sc(cs, PS_DAY + D_DGRAC, h) + gamma * r;
           return FV<2>{{PM, R}};
@@ -896,15 +890,17 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
         },
         cc, cs1);
     const float LEf = cc.v[0] * c2.v[0] + cs1.v[0] * s2.v[0];
-    const float VDD0f = DC(D_VDD) + ddiv((DC(D_A1) - DC(D_DG) * LEf) * DC(D_RAA), cs.day_r(DR_RHOCP));
+    const float VDD0f = DC(D_VDD) + ddiv((DC(D_A1) - DC(D_DG) * LEf) * DC(D_RAA), DC(D_RHOCP),
+                                              [&]() { return cs.day_r(DR_RHOCP); });
     FV<1> ft, fe;
     sp.template pick<1>(
         [&](int h) __attribute__((always_inline)) -> FV<1> {
           const float r = sel(h, rscf, rss);
-          const double rr = sp.own_day_rp(cs, DRP_RA, h);
-          const float LEh = mdiv(sp.own_sc(cs, PS_DAY + D_DRR, h) + ddiv(DC(D_RHOCP) * VDD0f, rr),
-                                 desatdT + gamma * (1.0f + ddiv(r, rr)));
-          return FV<1>{{ddiv(LEh * 1.0E3f, cs.day_r(DR_RL))}};
+          const float d = sp.own_sc(cs, PS_DAY + D_RAC, h);
+          auto rr = [&]() __attribute__((always_inline)) { return sp.own_day_rp(cs, DRP_RA, h); };
+          const float LEh = mdiv(sp.own_sc(cs, PS_DAY + D_DRR, h) + ddiv(DC(D_RHOCP) * VDD0f, d, rr),
+                                 desatdT + gamma * (1.0f + ddiv(r, d, rr)));
+          return FV<1>{{ddiv(LEh * 1.0E3f, DC(D_RL), [&]() { return cs.day_r(DR_RL); })}};
         },
         ft, fe);
 #if defined(H9G_FORCE_RERUN)   // test builds: the exact block in about one wave-substep of two
@@ -1076,10 +1072,16 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           if (inl_all || any_lane(inl)) {
           H9G_BR(BR_INL);
           const float d0 = zw - zlo;
+#if H9G_INL_MDIV
+          bool bq = false;
+          const float q1 = mk_div(O(PF_PTE), d0, bq);
+#else
           const float q1 = m.div_d(O(PF_PTE), d0, recip64(d0));
+          const bool bq = m.div_bad(q1);
+#endif
           const float voleq1 = q1 * (one - temp0);
           vin = m.div_d(voleq1 * (zw - zlo) + ts * (zhi - zw), zhi - zlo, cs.rdz_t(il));
-          bad |= inl && (m.div_bad(q1) | m.div_bad(vin));
+          bad |= inl && (bq | m.div_bad(vin));
           vin = MINF(ts, vin);
           vin = MAXF(vin, zero);
           }
@@ -1165,7 +1167,10 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
           float sm = O(PF_PSI) * ps;
           sm = MAXC(smpmin, sm);
           r.v[2] = sm;
-          r.v[3] = (-bsw) * sm / (s_node * ts);
+          if constexpr (H9G_HK_MDIV && L <= 8)
+            r.v[3] = mk_div((-bsw) * sm, s_node * ts, bad);   // dsmpdw, flagged for hk_exact
+          else
+            r.v[3] = (-bsw) * sm / (s_node * ts);
           return r;
     };
     auto hk_fast = [&](int t, int h, bool &bad) __attribute__((always_inline)) -> FV<4> {

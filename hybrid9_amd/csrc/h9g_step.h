@@ -168,6 +168,29 @@ H9K_HD bool bad_quotient(float q) {
 #endif
 }
 
+// x / d by the refined hardware reciprocal, y = fma(fma(-d, r, 1), r, r),
+// r = v_rcp_f32(d), and Markstein's correction of RN(x y): the correctly
+// rounded quotient for every pair of float significands
+// (tools/markstein_exhaustive.hip mode 1), so whenever |x| and |d| lie in
+// [2^-60, 2^60), where scaling by powers of two is exact; other operands
+// (x = 0 among them) set bad, for the caller's exact path.  Six dependent
+// operations against the IEEE division's nine.  (The host build uses the
+// correctly rounded 1/d, mode 0 of the same proof.)
+H9K_HD float mk_div(float x, float d, bool &bad) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float r = __builtin_amdgcn_rcpf(d);
+#else
+  const float r = 1.0f / d;
+#endif
+  const float y = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
+  const float q0 = x * y;
+  const float q = __builtin_fmaf(__builtin_fmaf(-d, q0, x), y, q0);
+  const uint32_t ux = (__builtin_bit_cast(uint32_t, x) & 0x7fffffffu) - 0x21800000u;   // 2^-60
+  const uint32_t ud = (__builtin_bit_cast(uint32_t, d) & 0x7fffffffu) - 0x21800000u;
+  bad |= (ux > ud ? ux : ud) >= 0x5d800000u - 0x21800000u;                             // 2^60
+  return q;
+}
+
 // Reciprocal of a float divisor in double, |r - 1/d| <= 1.2 * 2^-53 |1/d|:
 // hardware estimate + two Newton steps (each squares the error and adds
 // <= 2^-53; two steps suffice from any estimate within 2^-14).  NaN for

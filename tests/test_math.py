@@ -164,13 +164,17 @@ def test_markstein_quotient_of_conductivity_phase(tmp_path):
 
 
 @pytest.mark.gpu
-def test_markstein_quotient_exhaustive_slice_on_gpu():
+@pytest.mark.parametrize("mode", [0, 1])
+def test_markstein_quotient_exhaustive_slice_on_gpu(mode):
     """The exhaustive proof of hk_fast's s1 quotient (tools/markstein_exhaustive.hip:
     every pair of float significands, 7.04e13 pairs, 0 mismatches on the
     MI355X, profiles/markstein_r04.txt) re-run on the slice ADVICE r03 named:
     the 65,536 divisors whose significand is nearest all-ones, against every
     dividend significand (5.5e11 pairs), plus the one-ulp-off control that
-    must fail."""
+    must fail.  Mode 1 is the refined v_rcp_f32 reciprocal of mk_div
+    (h9g_step.h: the energy balance's and the conductivity phase's runtime
+    divisors, round 5; full sweep in profiles/markstein_rcp_r04.txt), with
+    its check of v_rcp_f32's scale invariance over [2^-60, 2^60)."""
     from tests.helpers import BUILD, ROOT, _build
     src = ROOT / "tools" / "markstein_exhaustive.hip"
     exe = ROOT / "tools" / "_build" / "markstein_exhaustive"
@@ -178,7 +182,7 @@ def test_markstein_quotient_exhaustive_slice_on_gpu():
         exe.parent.mkdir(exist_ok=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off",
                         "-fhip-fp32-correctly-rounded-divide-sqrt", "-o", str(exe), str(src)], check=True)
-    r = subprocess.run([str(exe), str((1 << 23) - (1 << 16)), str(1 << 23)], capture_output=True, text=True,
-                       timeout=120)
+    r = subprocess.run([str(exe), str((1 << 23) - (1 << 16)), str(1 << 23), str(mode)], capture_output=True,
+                       text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches against the IEEE quotient: 0" in r.stdout, r.stdout

@@ -71,7 +71,8 @@ __global__ void __launch_bounds__(256) mk_kernel(uint32_t b0, uint32_t bend, int
 
 // Mode 1 checks significands only, which is complete if the hardware
 // reciprocal is scale-invariant: v_rcp_f32(b 2^k) = v_rcp_f32(b) 2^-k for
-// every b significand and every k with b 2^k in [2^-60, 2^60).  Counted here.
+// every b significand and every k with b 2^k in [2^-60, 2^60), and odd in b
+// (the corrections are exact under a sign change of a or b).  Counted here.
 __global__ void __launch_bounds__(256) rcp_scale_kernel(unsigned *cnt) {
   const uint32_t mb = blockIdx.x * blockDim.x + threadIdx.x;
   if (mb >= NA) return;
@@ -82,6 +83,8 @@ __global__ void __launch_bounds__(256) rcp_scale_kernel(unsigned *cnt) {
     const float bk = __uint_as_float((uint32_t)((int)__float_as_uint(b) + (k << 23)));
     const uint32_t rk = __float_as_uint(__builtin_amdgcn_rcpf(bk));
     bad += rk != (uint32_t)((int)r - (k << 23)) ? 1u : 0u;
+    // and sign symmetry, v_rcp_f32(-b) = -v_rcp_f32(b) (mk_div takes signed operands)
+    bad += __float_as_uint(__builtin_amdgcn_rcpf(-bk)) != (rk ^ 0x80000000u) ? 1u : 0u;
   }
   cnt[mb] = bad;
 }
