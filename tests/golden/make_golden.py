@@ -437,6 +437,31 @@ def cell_order_blocks_case(name, gid, nx, ny, num_procs, *, year0=1901, nyears=2
     print(f"{name}: {gid.size} cells in {len(set(rank.tolist()))} blocks x {nyears} yr, vs one rank {vs_one}")
 
 
+def cell_order_stop_case(name="co_stop", year0=1901, nisurf=24, grow_on=1):
+    """A reference STOP inside the reference's own cell order: stop_ns24's
+    hand-built soils run by h9ref's cell_order mode (smp carried from cell to
+    cell).  The fixture is the STOP the reference prints (site, cell, day,
+    value); the inputs are stop_ns24's, regenerated here."""
+    land = synth.land_cells()
+    gid = np.asarray(land[263::527][90:98], dtype=np.int64)
+    p = independent_layer_params(gid)
+    f = synth.make_forcing(gid, synth.cell_lat(gid), synth.year_day0(year0), 365)
+    try:
+        refcase.run_case(cell_order=True, zi=synth.ZI_L8, params=p, forcing=f, nisurf=nisurf, year0=year0,
+                         nyears=1, grow_on=grow_on)
+    except refcase.RefStop as e:
+        info = e.info
+    else:
+        raise SystemExit(f"{name}: expected a reference STOP")
+    meta = dict(name=name, kind="cell_order_stop", L=8, ncell=int(gid.size), year0=year0, nyears=1,
+                nisurf=nisurf, grow_on=grow_on, zi=synth.ZI_L8.tolist(), stop=info, gid=gid.tolist(),
+                input_sha256=digest(packed_params(p), f),
+                generator="oracle/_ref/h9ref cell_order=1 STOP output")
+    np.savez_compressed(OUT / f"{name}.npz", meta=np.array(json.dumps(meta)),
+                        params=packed_params(p), forcing=f)
+    print(f"{name}: reference STOP in cell order {info}")
+
+
 def main_cell_order():
     g10 = np.array([(80 + j) * synth.NX05 + 400 + i for j in range(10) for i in range(10)])
     # config 1's grid over three decades (1901-1930)
@@ -447,6 +472,7 @@ def main_cell_order():
     cell_order_case("co_band", land[(rows >= 150) & (rows < 158)], nyears=20)
     # config 1's grid as the reference runs it on 4 MPI ranks (2 x 2 blocks of 5 x 5)
     cell_order_blocks_case("co_c1_blocks4", g10, 10, 10, 4)
+    cell_order_stop_case()
 
 
 def site_inputs(gid, L, nisurf, years, events, seed=synth.SEED, soils="synth", ppt_scale=1.0):

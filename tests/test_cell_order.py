@@ -188,3 +188,44 @@ def test_gpu_isolated_contract_bound(name):
           f"{diff} of {meta['ncell']} cells not bitwise")
     assert bound == rec["annual"] and diff == rec["cells_differing"]
     assert same_bits(a[:10], b[:10]) == rec["first_decade_bitwise"]
+
+
+def _stop_of(err):
+    return {k: int(err[k]) for k in ("code", "cell", "day")}
+
+
+def test_oracle_cell_order_reproduces_reference_stop():
+    """A STOP inside the reference's order (co_stop: the reference's
+    cell_order run of stop_ns24's soils, HYDROLOGY.f90:1244-1274): the
+    oracle's restatement stops with the reference's site, cell and day, and
+    the value it prints."""
+    from oracle import port
+    meta, inp, _ = load_golden("co_stop")
+    s = meta["stop"]
+    out = port.run_cell_order(**inp)
+    assert out["rc"] == s["code"]
+    assert _stop_of(out["err"]) == {k: s[k] for k in ("code", "cell", "day")}
+    assert np.float32(out["err"]["value"]) == np.float32(s["value"])
+
+
+@pytest.mark.gpu
+def test_gpu_cell_order_reproduces_reference_stop():
+    """The product in the reference's order (h9g_run_decade_ordered) returns
+    the reference's STOP (site, cell, day, printed value) as the first
+    failing cell in its order, and every cell that completes has the
+    oracle's annual sums bit for bit."""
+    import hybrid9_amd as h
+    from oracle import port
+    meta, inp, _ = load_golden("co_stop")
+    s = meta["stop"]
+    out = h.run_cell_order(**inp)
+    assert out["rc"] == s["code"], out["err"]
+    e = out["err"]
+    assert (int(e["cell"]), int(e["day"])) == (s["cell"], s["day"])
+    assert np.float32(e["value"]) == np.float32(s["value"])
+    ref = port.run_cell_order(**inp)
+    assert int(e["substep"]) == int(ref["err"]["substep"])      # not printed by the reference
+    ok = np.isfinite(ref["annual"]).all(axis=(0, 1))
+    assert not ok[s["cell"]] and ok.sum() == meta["ncell"] - 1
+    assert np.array_equal(np.isfinite(out["annual"]).all(axis=(0, 1)), ok)
+    assert same_bits(out["annual"][:, :, ok], ref["annual"][:, :, ok])
