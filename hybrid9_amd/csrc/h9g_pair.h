@@ -98,6 +98,9 @@ static_assert((PS_DAY + D_NUMC) % 2 == 0 && (PS_DAY + D_RAARAC) % 2 == 0 && (PS_
 #ifndef H9G_INL_MDIV
 #define H9G_INL_MDIV 0   // the in-layer case's PTE / (zw - zlo) by Markstein (eq_body) instead of recip64
 #endif
+#ifndef H9G_WT_DEFER
+#define H9G_WT_DEFER 1   // the water-table loops' x/1000 flag the substep's exact re-run (hydrology_pair; round 5: -0.45%)
+#endif
 #ifndef H9G_AQ_FREE
 #define H9G_AQ_FREE 0    // the aquifer node's second round and interface branch-free (hydrology_pair)
 #endif
@@ -1685,6 +1688,19 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
   // first visit's from the pick above); rous = s_y(L) of the pre-update
   // zwtmm came from the pair split of the equilibrium profile.
   float rous = MAXX(TS(L) * (one - pY.v[0]), 0.02f);
+  // x / 1000 in the water-table loops, which run only for a substep that
+  // started with the water table in the column (a day snapshot exists): a
+  // quotient that needs the IEEE division (subnormal) asks for the exact
+  // re-run of the substep instead of a redo branch in place (H9G_WT_DEFER)
+  auto wdiv = [&](float x) __attribute__((always_inline)) {
+    if constexpr (H9G_WT_DEFER && !M::kExact) {
+      const float q = m.div_d(x, 1000.0f, r1000);
+      m.special |= m.div_bad(q);
+      return q;
+    } else {
+      return m.div(x, 1000.0f, r1000);
+    }
+  };
   int jwt2 = jwt;
   if (jwt == L) {
     s.wa = s.wa + qcharge * dt;
@@ -1697,7 +1713,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
         const float s_y = k == 0 ? sy_first : s_y_at(i, zwtmm);
         float qcl = MINF(qcharge_tot, s_y * (zwtmm - cs.zi(i - 1)));
         qcl = MAXF(qcl, zero);
-        if (s_y > zero) s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
+        if (s_y > zero) s.zwt = s.zwt - wdiv(qcl / s_y);
         qcharge_tot = qcharge_tot - qcl;
         return !(qcharge_tot <= zero || i == 1);
       });
@@ -1709,7 +1725,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
         qcl = MINF(qcl, zero);
         qcharge_tot = qcharge_tot - qcl;
         if (qcharge_tot >= zero) {
-          s.zwt = s.zwt - m.div(qcl / s_y, 1000.0f, r1000);
+          s.zwt = s.zwt - wdiv(qcl / s_y);
           return false;
         }
         s.zwt = cs.zim(i);
@@ -1717,7 +1733,7 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
       });
       if (qcharge_tot > zero) {
         if (!aq) rous = s_y_at(L, zwtmm);    // this lane's first round was the recharge's
-        s.zwt = s.zwt - m.div(qcharge_tot, 1000.0f, r1000) / rous;
+        s.zwt = s.zwt - wdiv(qcharge_tot) / rous;
       }
     }
     jwt2 = jwt_of<L>(s.zwt, zim);
@@ -1775,13 +1791,13 @@ H9K_HD int hydrology_pair(const G &g, CS cs, const SP &sp0, St<L> &s, float &rnf
       }
       rsub_top_tot = rsub_top_tot - rstl;
       if (rsub_top_tot >= zero) {
-        s.zwt = s.zwt - m.div(rstl / s_y, 1000.0f, r1000);
+        s.zwt = s.zwt - wdiv(rstl / s_y);
         return false;
       }
       s.zwt = cs.zim(i);
       return i != L;
     });
-    s.zwt = s.zwt - m.div(rsub_top_tot, 1000.0f, r1000) / rous;
+    s.zwt = s.zwt - wdiv(rsub_top_tot) / rous;
     s.wa = s.wa + rsub_top_tot;
     jwt3 = jwt_of<L>(s.zwt, zim);
   }
