@@ -4,9 +4,18 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload config2]
 
 A *step* is one simulated calendar year for every land cell of the GPU:
-365/366 days x NISURF substeps of HYDROLOGY (+ daily GROW when enabled),
-i.e. one ``h9g_run_year`` launch, followed by the per-year FP64 diagnostics
-that are all-reduced across GPUs over RCCL (torch.distributed "nccl").
+365/366 days x NISURF substeps of HYDROLOGY (+ daily GROW when enabled).
+By default (``--order cell``, round 6) the years run in the reference's own
+order -- decade -> cell -> year, smp carried from cell to cell
+(HYBRID9.f90:93-130), bit-identical to the reference -- as one
+``h9g_run_ordered`` call over whole reference decades: the untimed warm-up
+is rounded up to whole decades (``--warmup 5`` runs 1901-1910) and the
+timed years must be whole decades (``--steps 20``: 1911-1930).
+``--order isolated`` times ``h9g_run_year`` launches (every cell its own
+smp, the contract of rounds 1-5; it misses the reference by up to 4e-2,
+DESIGN.md §2); the default run reports it under ``isolated``.  The FP64
+diagnostics are all-reduced across GPUs over RCCL (torch.distributed
+"nccl") after each call (cell order) or year (isolated).
 Inputs (soil parameters, a distinct forcing year per step) are generated on
 the device and resident in HBM before the timed region.  Weak scaling (the
 default): each rank simulates the full synthetic land grid with its own seed;
@@ -14,9 +23,12 @@ default): each rank simulates the full synthetic land grid with its own seed;
 Rank 0 prints one JSON line.
 
 ``value`` = cell-steps/s over all ranks (cells x days x NISURF x K / max
-rank time).  ``roofline.achieved`` = the SURVEY.md §8d algorithmic bytes of
-the per-substep SHARED-state contract (4(10L+14) B/cell-step) per launch /
-the launch's device time from HIP events on the kernel's stream.
+rank time; re-runs of the cell order are overhead, not counted).
+``roofline.achieved`` = the SURVEY.md §8d algorithmic bytes of the
+per-substep SHARED-state contract (4(10L+14) B/cell-step) per launch of the
+dominant kernel (the pair kernel: the cell order's year launches and their
+riding re-runs, and its year-1 re-runs) / the launch's device time from HIP
+events on the kernel's stream.
 ``cpu_baseline`` times the reference itself (oracle/_ref/h9ref: unmodified
 HYDROLOGY.f90 compiled with amdflang) on a bounded sample of the same
 workload, one process per host core, rank 0 at N=1 only.
@@ -158,12 +170,31 @@ def cpu_baseline(workload: dict, seed: int) -> dict:
         ok = True
     steps = P * C * nt * ns
     subprocess.run(["rm", "-rf", str(tmp)])
-    return {"value": steps / wall, "unit": "cell-steps/s", "cores": P, "kind": kind,
+    return {"value": steps / wall, "unit": "cell-steps/s", "cores": P, "kind": kind, "host": host_cpu(),
             "sample": f"{'reference HYDROLOGY.f90 (amdflang -O2)' if kind == 'reference' else 'C port'}"
                       f"{'' if L == 8 else ' rebuilt with nsoil_layers_max=10'}"
                       f" x {P} processes x {C} cells x 1 yr ({ns} substeps/day, GROW "
                       f"{'on' if grow else 'off'}, L={L}) = {steps:.3e} cell-steps in {wall:.1f} s"
                       f"{'' if ok else ' (a sample process STOPped)'}"}
+
+
+def host_cpu() -> dict:
+    """The box's host CPU as this process sees it: os.cpu_count(), the
+    affinity mask's size (the lease) and the model (/proc/cpuinfo)."""
+    model = None
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"cpu_count": os.cpu_count(), "usable": usable, "model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def load_traffic(workload_name: str, kernel: str, build: str | None = None, root: Path = ROOT):
@@ -401,54 +432,68 @@ def diag_exchange(ctx, torch, dist, device: str):
 
 
 def ordered_years(ctx, pl: dict, s0: int, s1: int, exchange, work: list) -> None:
-    """Steps s0 .. s1-1 in the reference's own cell order: the reference's
-    decades (HYBRID9.f90:93-130) cut to the range, one
-    h9g_run_decade_ordered each (smp carried from cell to cell)."""
-    import hybrid9_amd as h
+    """Steps s0 .. s1-1, whole reference decades (HYBRID9.f90:93-130), as
+    one h9g_run_ordered call: the decades overlap on the device and every
+    year's forcing stays resident."""
     if s1 <= s0:
         return
-    for y0, ny in h.decades(pl["years"][s0], s1 - s0):
-        s = pl["years"].index(y0)
-        ctx.run_decade_ordered([pl["slot_of_step"][k] for k in range(s, s + ny)], y0, raise_on_stop=False,
-                               annual=False)
-        work.append(dict(ctx.decade_stats(), years=ny))
-        if exchange:
-            exchange()
+    ctx.run_ordered([pl["slot_of_step"][k] for k in range(s0, s1)], pl["years"][s0], raise_on_stop=False,
+                    annual=False)
+    work.append(dict(ctx.decade_stats(), overlap=ctx.ordered_stats(), years=s1 - s0))
+    if exchange:
+        exchange()
 
 
-def cell_order_line(ctx, pl: dict, ns: int, sync) -> dict:
-    """The same cells in the reference's own cell order (h9g_run_decade_ordered),
-    after the main measurement: the state re-initialised, decade 1901-1910
-    untimed, decade 1911-1920 timed (steps 0-19 of the ring).  A secondary
-    line: the main `value` is the isolated-cell path."""
+def decade_aligned(W: int, K: int) -> tuple[int, int]:
+    """The cell order's warm-up and timed years: the warm-up rounded up to
+    whole decades from 1901; the timed years must be whole decades, since a
+    cut decade is not the reference's order (a cell's successor would start
+    from its smp in the middle of the decade)."""
+    if K < 10 or K % 10:
+        raise SystemExit(f"--order cell times whole reference decades: --steps {K} is not a multiple of 10 "
+                         "(use --order isolated for other counts)")
+    return (W + 9) // 10 * 10, K
+
+
+def isolated_line(ctx, pl: dict, ns: int, sync, W: int = 5, K: int = 20) -> dict:
+    """The isolated-cell contract (h9g_run_year: every cell its own smp,
+    rounds 1-5's `value`) on the same cells after the main measurement: the
+    state re-initialised, W years untimed, K timed.  Secondary: it misses
+    the reference's order by up to 4e-2."""
     from hybrid9_amd import synth
     ctx.init_state()
-    sub = dict(pl, W=10, K=10, years=pl["years"][:20], slot_of_step=pl["slot_of_step"][:20])
-    work = []
-    el = timed_steps(ctx, sub, None, sync, "cell", work)
+    W, K = min(W, len(pl["years"]) - 1), min(K, len(pl["years"]))
+    W = min(W, len(pl["years"]) - K)
+    sub = dict(pl, W=W, K=K, years=pl["years"][:W + K], slot_of_step=pl["slot_of_step"][:W + K])
+    ctx.launch_stats(reset=True)
+    el = timed_steps(ctx, sub, None, sync, "isolated")
     kern_ms = ctx.total_kernel_ms(reset=True)
     d = ctx.get_diagnostics()
     failed = int(round(float(d[11])))
-    steps = sum(synth.days_in_year(y) for y in sub["years"][10:]) * ns
+    steps = sum(synth.days_in_year(y) for y in sub["years"][W:]) * ns
     n = pl["gid"].size
-    return {"value": (n - failed) * steps / el, "unit": "cell-steps/s", "years": "1911-1920 timed (1901-1910 untimed)",
-            "ms_per_year": el / 10 * 1e3, "kernel_ms_per_year": kern_ms / 10, "decades": work,
-            "rerun_cell_years_per_cell_year": sum(w["rerun_cell_years"] for w in work) / float(n * 10),
-            "semantics": "the reference's decade -> cell -> year order, smp carried from cell to cell "
-                         "(bit-identical to the reference on one rank, DESIGN.md §2)"}
+    algo = (n - failed) * steps / K * bytes_per_cell_step(pl["L"])
+    return {"value": (n - failed) * steps / el, "unit": "cell-steps/s",
+            "years": f"{sub['years'][W]}-{sub['years'][-1]} timed ({W} untimed)",
+            "ms_per_step": el / K * 1e3, "kernel_ms_per_launch": kern_ms / K,
+            "roofline_frac": algo / (kern_ms / K / 1e3) / 1e9 / HBM_PEAK_GBS,
+            "semantics": "isolated cells (h9g_run_year, every cell its own smp): not the reference's order, "
+                         "up to 4e-2 relative from it (DESIGN.md §2)"}
 
 
 def timed_steps(ctx, pl: dict, exchange, sync, order: str = "isolated", work: list | None = None) -> float:
     """W untimed warmup years, then K timed years between two `sync`s
     (barrier + device synchronisation).  Returns the elapsed seconds.
-    order "cell": the years in the reference's cell order (ordered_years;
-    `work` collects each decade's h9g_decade_stats)."""
+    order "cell": the W and K years each as one h9g_run_ordered call
+    (ordered_years; `work` collects each call's stats); both whole decades."""
     W, K = pl["W"], pl["K"]
     if order == "cell":
         work = [] if work is None else work
         ordered_years(ctx, pl, 0, W, exchange, [])
         sync()
         ctx.total_kernel_ms(reset=True)
+        if hasattr(ctx, "launch_stats"):
+            ctx.launch_stats(reset=True)
         t0 = time.perf_counter()
         ordered_years(ctx, pl, W, W + K, exchange, work)
         sync()
@@ -471,8 +516,11 @@ def timed_steps(ctx, pl: dict, exchange, sync, order: str = "isolated", work: li
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="timed years (default 3; config4: 30)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed years (default 1; config4: 0)")
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed years (cell order: whole decades, default 20; isolated: default 3; config4: 30)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed years (cell order: rounded up to whole decades, default 10; isolated: default "
+                         "1; config4: 0)")
     ap.add_argument("--workload", default="config2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=None)
@@ -481,26 +529,34 @@ def main():
                          "a full grid per rank with seed + rank)")
     ap.add_argument("--host-fed", action="store_true",
                     help="PCIe-inclusive rate: every step's forcing year is copied from pinned host "
-                         "memory (async, double-buffered); reported in DESIGN.md, never as `value`")
-    ap.add_argument("--order", choices=["isolated", "cell"], default="isolated",
-                    help="cell: the reference's own cell order (h9g_run_decade_ordered per decade, smp "
-                         "carried from cell to cell, bit-identical to the reference); isolated: every cell "
-                         "its own smp (h9g_run_year per year)")
-    ap.add_argument("--no-cell-order-line", action="store_true",
-                    help="skip the secondary measurement of the reference's cell order (the default run "
-                         "adds it at N=1 when the ring holds 1901-1920: decade 1901-1910 untimed, "
-                         "1911-1920 timed, reported under cell_order, never as `value`)")
+                         "memory (async, double-buffered; isolated order); reported in DESIGN.md, never as `value`")
+    ap.add_argument("--order", choices=["isolated", "cell"], default=None,
+                    help="cell (default): the reference's own cell order (h9g_run_ordered over whole decades, "
+                         "smp carried from cell to cell, bit-identical to the reference); isolated: every cell "
+                         "its own smp (h9g_run_year per year; the default with --host-fed / --forcing nc4)")
+    ap.add_argument("--no-isolated-line", action="store_true",
+                    help="skip the secondary measurement of the isolated-cell contract (the default cell-order "
+                         "run at N=1 adds it: 1901-1905 untimed, 1906-1925 timed, reported under `isolated`, "
+                         "never as `value`)")
     ap.add_argument("--forcing", choices=["device", "nc4"], default="device",
                     help="nc4: every step's forcing is read from synthetic PGF netCDF-4 files through "
-                         "h9g_nc_forcing_prefetch (ingest-inclusive; DESIGN.md, never as `value`)")
+                         "h9g_nc_forcing_prefetch (ingest-inclusive, isolated order; DESIGN.md, never as `value`)")
     args = ap.parse_args()
     if args.forcing == "nc4" and (args.host_fed or WORKLOADS[args.workload]["grid"] != "05"):
         raise SystemExit("--forcing nc4: 0.5 deg workloads only, not with --host-fed")
-    if args.order == "cell" and (args.host_fed or args.forcing != "device"):
-        raise SystemExit("--order cell: resident device forcing only")
+    streamed = args.host_fed or args.forcing != "device"
+    if args.order is None:
+        args.order = "isolated" if streamed else "cell"
+    if args.order == "cell" and streamed:
+        raise SystemExit("--order cell: resident device forcing only (every year of a call stays resident)")
     wl = WORKLOADS[args.workload]
-    K = args.steps if args.steps is not None else wl.get("steps", 3)
-    W = args.warmup if args.warmup is not None else wl.get("warmup", 1)
+    if args.order == "cell":
+        K = args.steps if args.steps is not None else wl.get("steps", 20)
+        W_req = args.warmup if args.warmup is not None else wl.get("warmup", 10)
+        W, K = decade_aligned(W_req, K)
+    else:
+        K = args.steps if args.steps is not None else wl.get("steps", 3)
+        W_req = W = args.warmup if args.warmup is not None else wl.get("warmup", 1)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # launched without torchrun: start one rank per GPU as child processes
@@ -566,10 +622,22 @@ def main():
     work = []
     elapsed = timed_steps(runner, pl, exchange, sync, args.order, work)
     kern_ms = ctx.total_kernel_ms(reset=True)
+    launches = ctx.launch_stats(reset=True)
+    # the dominant kernel's launches: in cell order the context's pair kernel
+    # (every year launch of the first passes, with the re-runs riding in them,
+    # and the year-1 re-runs); the one-column kernel of short re-run lists
+    # is reported beside it
+    kname = ctx.kernel_name()
+    main_kind = {1: "pair", 2: "solo", 3: "mixed", 4: "pair2", 5: "pair11"}[ctx.kind_id()]
+    if args.order == "cell" and main_kind in launches:
+        ml = launches[main_kind]
+        n_launch, launch_ms, cy_launch = ml["launches"], ml["ms"], ml["cell_years"] / max(1, ml["launches"])
+    else:
+        n_launch, launch_ms, cy_launch = K, kern_ms, None
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, kern_ms, launch_ms], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        elapsed, kern_ms, launch_ms = float(t[0]), float(t[1]), float(t[2])
         diag = diag_t.cpu().numpy()
     else:
         diag = ctx.get_diagnostics()
@@ -580,8 +648,11 @@ def main():
     steps_per_cell = sum(synth.days_in_year(y) * ns for y in years[W:])
     cell_steps_rank = (n_total - failed) / world * steps_per_cell
     value = (n_total - failed) * steps_per_cell / elapsed
-    launch_s = kern_ms / 1e3 / K
-    algo_bytes_launch = cell_steps_rank / K * bytes_per_cell_step(L)
+    launch_s = launch_ms / 1e3 / n_launch
+    if cy_launch is None:
+        algo_bytes_launch = cell_steps_rank / K * bytes_per_cell_step(L)
+    else:      # cell-years of an average launch x the timed years' mean substeps per cell-year
+        algo_bytes_launch = cy_launch * steps_per_cell / K * bytes_per_cell_step(L)
     achieved = algo_bytes_launch / launch_s / 1e9
     build = h.build_id()
     pmc, stale = load_traffic(args.workload, ctx.kernel_name(), build)
@@ -596,7 +667,7 @@ def main():
         "unit": "cell-steps/s",
         "n_gpus": world,
         "steps": K,
-        "warmup": W,
+        "warmup": W_req,
         "ms_per_step": elapsed / K * 1e3,
         "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak",
@@ -608,13 +679,16 @@ def main():
         "config": {"workload": f"{args.workload}: {wl['desc']}", "cells_per_gpu": int(gid.size),
                    "cells_total": int(n_total),
                    "nlayers": L, "nisurf": ns, "grow": wl["grow_on"],
-                   "years_per_step": 1, "years": f"{years[W]}-{years[-1]} timed",
+                   "years_per_step": 1,
+                   "years": f"{years[W]}-{years[-1]} timed" + (f", {years[0]}-{years[W - 1]} untimed" if W else ""),
+                   "order": args.order,
                    "forcing_slots": nslots,
                    "parallelism": f"dp{world} (cell shards, RCCL all-reduce "
                    "of FP64 diagnostics per year)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ctx.kernel_name(), "kernel_ms_per_launch": launch_s * 1e3,
+                     "kernel": kname, "kernel_ms_per_launch": launch_s * 1e3, "launches": n_launch,
+                     "cell_years_per_launch": cy_launch if cy_launch is not None else (n_total - failed) / world,
                      "algorithmic_bytes_per_launch": algo_bytes_launch,
                      "traffic_source": (pmc or {}).get("source"), "valu": valu,
                      "build_id": build, "traffic_stale": stale,
@@ -624,14 +698,20 @@ def main():
         "diagnostics_last_year": {k: float(v) for k, v in zip(h.DIAG_NAMES, diag)},
         "cells_stopped": failed,
         "order": args.order,
+        "semantics": ("the reference's own order: decade -> cell -> year, smp carried from cell to cell "
+                      "(HYBRID9.f90:93-130), bit-identical to the reference (DESIGN.md §2)"
+                      if args.order == "cell" else
+                      "isolated cells (every cell its own smp): not the reference's order (DESIGN.md §2)"),
+        "kernel_ms_total": kern_ms,
+        "launches": launches,
     }
     if args.order == "cell":
-        out["cell_order"] = {"decades": work,
+        out["cell_order"] = {"calls": work,
                              "rerun_cell_years_per_cell_year": sum(w["rerun_cell_years"] for w in work) /
-                             max(1.0, float(gid.size * K))}
-    elif (world == 1 and host_fed is None and nc_fed is None and not args.no_cell_order_line
-          and len(pl["years"]) >= 20):
-        out["cell_order"] = cell_order_line(ctx, pl, ns, sync)
+                             max(1.0, float(gid.size * K)),
+                             "warmup_years_run": W}
+        if (world == 1 and not args.no_isolated_line and len(pl["years"]) >= 25):
+            out["isolated"] = isolated_line(ctx, pl, ns, sync)
     if host_fed is not None:
         out["host_fed"] = host_fed.describe()
         host_fed.close()

@@ -104,7 +104,10 @@ def lib() -> C.CDLL:
         "h9g_run_year": (C.c_int, [vp, C.c_int, C.c_int]),
         "h9g_run_decade_ordered": (C.c_int, [vp, C.POINTER(C.c_int32), C.c_int, C.c_int, _FP,
                                              C.POINTER(C.c_int32)]),
+        "h9g_run_ordered": (C.c_int, [vp, C.POINTER(C.c_int32), C.c_int, C.c_int, _FP, C.POINTER(C.c_int32)]),
         "h9g_decade_stats": (C.c_int, [vp, C.POINTER(C.c_int64), C.c_int]),
+        "h9g_ordered_stats": (C.c_int, [vp, C.POINTER(C.c_int64), C.c_int]),
+        "h9g_launch_stats": (C.c_int, [vp, _DP, C.c_int, C.c_int]),
         "h9g_set_chains": (C.c_int, [vp, C.POINTER(C.c_int32)]),
         "h9g_sync": (C.c_int, [vp]),
         "h9g_last_error": (C.c_int, [vp, C.POINTER(_Error)]),
@@ -360,6 +363,42 @@ class Context:
             raise ReferenceStop(self.last_error())
         return out, int(np_.value)
 
+    def run_ordered(self, slots, jyear0: int, raise_on_stop: bool = True, annual: bool = True):
+        """Years jyear0 .. jyear0+len(slots)-1 in the reference's own cell
+        order, cut into its decades, which overlap on the device
+        (h9g_run_ordered; bit-identical to run_decade_ordered per decade);
+        synchronous.  Every year's slot must stay resident for the call.
+        Returns (annual (nyears, 12+L, ncell) or None, passes per decade);
+        self.decade_rc holds the STOP code."""
+        sl = np.ascontiguousarray(slots, dtype=np.int32)
+        out = np.empty((sl.size, 12 + self.L, self.ncell), dtype=np.float32) if annual else None
+        np_ = (C.c_int32 * max(1, len(decades(jyear0, sl.size))))()
+        rc = _check(self._lib.h9g_run_ordered(self._h, sl.ctypes.data_as(C.POINTER(C.c_int32)), jyear0, sl.size,
+                                              _fp(out) if annual else None, np_), "h9g_run_ordered")
+        self.decade_rc = rc
+        if rc and raise_on_stop:
+            raise ReferenceStop(self.last_error())
+        return out, [int(v) for v in np_][:len(decades(jyear0, sl.size))]
+
+    def ordered_stats(self) -> dict:
+        """How the last ordered call overlapped its decades (h9g_ordered_stats)."""
+        out = (C.c_int64 * 64)()
+        m = _check(self._lib.h9g_ordered_stats(self._h, out, 64), "h9g_ordered_stats")
+        keys = ("decades", "first_pass_launches", "rerun_years_riding", "rerun_cell_years_riding",
+                "rerun_years_alone", "rerun_cell_years_alone")
+        d = {k: int(out[i]) for i, k in enumerate(keys)}
+        d["passes"] = [int(out[i]) for i in range(6, m)]
+        return d
+
+    def launch_stats(self, reset: bool = False) -> dict:
+        """Year launches per kernel kind since the last reset
+        (h9g_launch_stats): launches, cell-years, device ms."""
+        out = (C.c_double * 18)()
+        m = _check(self._lib.h9g_launch_stats(self._h, out, 18, int(reset)), "h9g_launch_stats")
+        names = ("pair", "solo", "mixed", "pair2", "pair11", "pair1")
+        return {nm: dict(launches=int(out[3 * i]), cell_years=int(out[3 * i + 1]), ms=float(out[3 * i + 2]))
+                for i, nm in enumerate(names) if 3 * i + 2 < m and out[3 * i] > 0}
+
     def set_chains(self, chain=None):
         """Independent cell-order chains, one per reference rank
         (h9g_set_chains; shard.reference_blocks gives the reference's).
@@ -449,6 +488,17 @@ class Context:
     def kernel_name(self) -> str:
         return self._lib.h9g_kernel_name(self._h).decode()
 
+    def kind_id(self) -> int:
+        """The context's year kernel as h9g_launch_stats numbers it: 1 pair,
+        2 solo, 3 solo rounds + pair, 4 pair2, 5 pair11."""
+        name = self.kernel_name()
+        if "+" in name:
+            return 3
+        for prefix, k in (("h9g_solo_", 2), ("h9g_pair2_", 4), ("h9g_pair11_", 5)):
+            if name.startswith(prefix):
+                return k
+        return 1
+
 
 PGF_VARS = ("tas", "rlds", "rsds", "huss", "ps", "pr", "rhs")   # READ_PGF.f90 order
 
@@ -515,14 +565,43 @@ def decades(year0: int, nyears: int):
 
 
 def run_cell_order(*, zi, params, forcing, nisurf=48, year0=1901, nyears=1, grow_on=True,
-                   state0: np.ndarray | None = None, device=0, chains=None):
-    """``run`` in the reference's own cell order: decade by decade through
-    ``Context.run_decade_ordered`` (smp carried from cell to cell, cells in
-    the given order; chains: a reference rank per cell, each rank its own
-    chain, shard.reference_blocks).  Returns dict(annual, state, rc, err,
-    errors, passes (per decade), work (decade_stats per decade))."""
+                   state0: np.ndarray | None = None, device=0, chains=None, pipelined=True):
+    """``run`` in the reference's own cell order (smp carried from cell to
+    cell, cells in the given order; chains: a reference rank per cell, each
+    rank its own chain, shard.reference_blocks).  pipelined: one
+    ``Context.run_ordered`` over all the years (every year's forcing
+    resident, the decades overlapping on the device); else decade by decade
+    through ``Context.run_decade_ordered``.  Returns dict(annual, state, rc,
+    err, errors, passes (per decade), work (decade_stats per call),
+    overlap (ordered_stats, pipelined))."""
     L = params["theta_s"].shape[1]
     n = params["fmax"].size
+    with Context(n, zi, nlayers=L, nisurf=nisurf, grow_on=grow_on, device=device,
+                 nslots=nyears if pipelined else 10) as ctx:
+        ctx.set_chains(chains)
+        ctx.set_params(params)
+        if state0 is None:
+            ctx.init_state()
+        else:
+            ctx.set_state(state0)
+        ann = np.full((nyears, 12 + L, n), np.nan, dtype=np.float32)
+        d0, rc, err, passes, work = 0, 0, None, [], []
+        if pipelined:
+            for k in range(nyears):
+                nt = days_in_year(year0 + k)
+                ctx.push_forcing(k, forcing[:, d0:d0 + nt, :])
+                d0 += nt
+            a, passes = ctx.run_ordered(list(range(nyears)), year0, raise_on_stop=False)
+            rc = ctx.decade_rc
+            if not rc or len(decades(year0, nyears)) == 1:
+                return dict(annual=a, state=ctx.get_state(), rc=rc, err=ctx.last_error() if rc else None,
+                            errors=ctx.get_errors(), passes=passes, work=[ctx.decade_stats()],
+                            overlap=ctx.ordered_stats())
+    if pipelined:
+        # a STOP: the reference program ends in that decade, while run_ordered
+        # goes on with the other cells; the decade-by-decade form stops there
+        return run_cell_order(zi=zi, params=params, forcing=forcing, nisurf=nisurf, year0=year0, nyears=nyears,
+                              grow_on=grow_on, state0=state0, device=device, chains=chains, pipelined=False)
     with Context(n, zi, nlayers=L, nisurf=nisurf, grow_on=grow_on, device=device, nslots=10) as ctx:
         ctx.set_chains(chains)
         ctx.set_params(params)

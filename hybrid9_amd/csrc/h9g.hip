@@ -63,6 +63,10 @@ static const double h_log2tab[32] = H9M_POWF_LOG2_TAB_INIT;
 #define H9G_PLANES (2 * H9G_PCPW)
 #define H9G_PWAVES 4
 #define NEVT 64
+// Cells a year launch carries at most in its second group (KArgs::split);
+// the slot-ordered forcing and annual buffers have that much slack.
+#define H9G_G2_MAX 1024
+static size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
 // ---------------------------------------------------------------------------
 // kernel arguments
@@ -88,6 +92,16 @@ struct KArgs {
   unsigned *__restrict__ pace;     // pair kernel, Pacer mode 2: H9G_PACE_ROWS x 16 progress words
   unsigned epoch;                  // Pacer mode 2: launch tag
   int prio_mode;                   // Pacer mode: 0 none, 1 rotate, 2 pace
+  // A second group of cells in the same launch (pair kernels; the cell-order
+  // mode's re-runs of one decade riding in the next decade's year launches,
+  // h9g_run_ordered).  Slots [c0, bend) are the first group; the waves from
+  // slot `split` (a multiple of the wave's column count, >= bend) to cend
+  // the second, with their own state and error rows, year length and no
+  // sort history.  split == cend: no second group.
+  int bend, split, nt2;
+  float *__restrict__ st2;
+  int *__restrict__ err2;
+  size_t iostride;                 // row stride of forc and annual when sorted_io (slots)
 };
 
 // XCD-aware workgroup order.  MI355X deals the workgroups of a launch
@@ -148,15 +162,24 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   const bool spare = lane >= 2 * C;
   if (spare && !PS::kSpare) return;
   const int h = lane & 1;
-  const int slot0 = a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * C;
-  const int ncol = min(C, a.cend - slot0);
+  const int slot0 = __builtin_amdgcn_readfirstlane(
+      a.c0 + (int)(xcd_vwg(blockIdx.x, gridDim.x) * H9G_PWAVES + wave) * C);
+  // the wave's group (wave-uniform: split is a multiple of C)
+  const bool g2 = slot0 >= a.split;
+  const int lim = g2 ? a.cend : a.bend;
+  float *const st = g2 ? a.st2 : a.st;
+  int *const err = g2 ? a.err2 : a.err;
+  int *const hist = g2 ? nullptr : a.hist;
+  const int nt = g2 ? a.nt2 : a.nt;
+  const int ncol = min(C, lim - slot0);
   if (ncol <= 0) return;             // an empty wave
   const int pl = spare ? (lane - 2 * C + (C == H9G_PCPW ? 12 : 0)) % (2 * ncol) : lane;
   const int slot = slot0 + (pl >> 1);
-  if (slot >= a.cend) return;        // both lanes of a pair leave together
+  if (slot >= lim) return;           // both lanes of a pair leave together
   const int c = a.perm ? a.perm[slot] : slot;
   const int io = a.sorted_io ? slot : c;   // forcing and annual sums: slot order when sorted
   const int n = a.ncell;
+  const size_t ios = a.sorted_io ? a.iostride : (size_t)n;
 
   int prow, pslot;
   pace_key(prow, pslot);
@@ -174,22 +197,22 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
       for (int t = 0; t < L / 2; t++) cs.set_slot(p, t, a.par[(size_t)(p * L + 2 * t + h) * n + c]);
     cs.set_sc(PS_FMAX, a.par[(size_t)(4 * L) * n + c]);
 #pragma unroll
-    for (int t = 0; t < L / 2; t++) cs.set_slot(PF_ROOTR, t, a.st[(size_t)(3 * L + 2 * t + h) * n + c]);
+    for (int t = 0; t < L / 2; t++) cs.set_slot(PF_ROOTR, t, st[(size_t)(3 * L + 2 * t + h) * n + c]);
   }
 #pragma unroll
   for (int i = 1; i <= L; i++) {
-    s.h2o[i] = a.st[(size_t)(0 * L + i - 1) * n + c];
-    s.smp[i] = a.st[(size_t)(2 * L + i - 1) * n + c];
+    s.h2o[i] = st[(size_t)(0 * L + i - 1) * n + c];
+    s.smp[i] = st[(size_t)(2 * L + i - 1) * n + c];
   }
   const size_t o8 = (size_t)(4 * L + 1) * n + c;
-  s.zwt = a.st[o8 + 0 * (size_t)n];
-  s.wa = a.st[o8 + 1 * (size_t)n];
-  s.LAI = a.st[o8 + 2 * (size_t)n];
-  s.LAI_litter = a.st[o8 + 3 * (size_t)n];
-  s.pm = a.st[o8 + 4 * (size_t)n];
-  s.pfm = a.st[o8 + 5 * (size_t)n];
-  s.plen = a.st[o8 + 6 * (size_t)n];
-  s.rdepth = a.st[o8 + 7 * (size_t)n];
+  s.zwt = st[o8 + 0 * (size_t)n];
+  s.wa = st[o8 + 1 * (size_t)n];
+  s.LAI = st[o8 + 2 * (size_t)n];
+  s.LAI_litter = st[o8 + 3 * (size_t)n];
+  s.pm = st[o8 + 4 * (size_t)n];
+  s.pfm = st[o8 + 5 * (size_t)n];
+  s.plen = st[o8 + 6 * (size_t)n];
+  s.rdepth = st[o8 + 7 * (size_t)n];
   cs.launder();
 
   if (!spare) {
@@ -197,10 +220,10 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
     float ts_sum = zero;
 #pragma unroll
     for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.lay(PF_TS, i);
-    if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
+    if (!(ts_sum > 1.0E-8f) || err[c] != 0) {
       if (h == 0)
 #pragma unroll
-        for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + io] = __builtin_nanf("");
+        for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * ios + io] = __builtin_nanf("");
       return;
     }
     cell_inv_pair<L, G>(g, cs);
@@ -210,45 +233,45 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   float errval = 0.0f;
 #if defined(H9G_STAMPS)
   StampProf pr{stamp_clock(), {0, 0, 0, 0, 0, 0, 0, 0}};
-  const int code = cell_year_pair<L, G, Split2, PS, true>(g, cs, sp, s, (const gbl_float *)(a.forc + io), (size_t)n, a.fvar, a.nt,
-                                                         a.nisurf, a.grow_on, (gbl_float *)(a.annual + io), (size_t)n, eday,
+  const int code = cell_year_pair<L, G, Split2, PS, true>(g, cs, sp, s, (const gbl_float *)(a.forc + io), ios, a.fvar, nt,
+                                                         a.nisurf, a.grow_on, (gbl_float *)(a.annual + io), ios, eday,
                                                          estep, errval, T, pr);
   if (lane == 0 && a.stamps)
     for (int k = 0; k < 8; k++) a.stamps[(blockIdx.x * H9G_PWAVES + wave) * 8 + k] = pr.acc[k];
 #else
-  const int code = cell_year_pair<L, G>(g, cs, sp, s, (const gbl_float *)(a.forc + io), (size_t)n, a.fvar, a.nt, a.nisurf,
-                                        a.grow_on, (gbl_float *)(a.annual + io), (size_t)n, eday, estep, errval, T);
+  const int code = cell_year_pair<L, G>(g, cs, sp, s, (const gbl_float *)(a.forc + io), ios, a.fvar, nt, a.nisurf,
+                                        a.grow_on, (gbl_float *)(a.annual + io), ios, eday, estep, errval, T);
 #endif
   if (spare || h != 0) return;       // the even lane writes the cell back
   int cw = c, iow = io;
   opaque(cw);
   opaque(iow);
   cs.launder();
-  if (a.hist) a.hist[cw] = s.naq;
+  if (hist) hist[cw] = s.naq;
   const size_t ow = (size_t)(4 * L + 1) * n + cw;
 #pragma unroll
   for (int i = 1; i <= L; i++) {
-    a.st[(size_t)(0 * L + i - 1) * n + cw] = s.h2o[i];
-    a.st[(size_t)(2 * L + i - 1) * n + cw] = s.smp[i];
-    if (a.grow_on) a.st[(size_t)(3 * L + i - 1) * n + cw] = cs.lay(PF_ROOTR, i);
+    st[(size_t)(0 * L + i - 1) * n + cw] = s.h2o[i];
+    st[(size_t)(2 * L + i - 1) * n + cw] = s.smp[i];
+    if (a.grow_on) st[(size_t)(3 * L + i - 1) * n + cw] = cs.lay(PF_ROOTR, i);
   }
-  if (a.grow_on) a.st[(size_t)(4 * L) * n + cw] = zero;   // rootr_col(Nlevgrnd)
-  a.st[ow + 0 * (size_t)n] = s.zwt;
-  a.st[ow + 1 * (size_t)n] = s.wa;
-  a.st[ow + 2 * (size_t)n] = s.LAI;
-  a.st[ow + 3 * (size_t)n] = s.LAI_litter;
-  a.st[ow + 4 * (size_t)n] = s.pm;
-  a.st[ow + 5 * (size_t)n] = s.pfm;
-  a.st[ow + 6 * (size_t)n] = s.plen;
-  a.st[ow + 7 * (size_t)n] = s.rdepth;
+  if (a.grow_on) st[(size_t)(4 * L) * n + cw] = zero;   // rootr_col(Nlevgrnd)
+  st[ow + 0 * (size_t)n] = s.zwt;
+  st[ow + 1 * (size_t)n] = s.wa;
+  st[ow + 2 * (size_t)n] = s.LAI;
+  st[ow + 3 * (size_t)n] = s.LAI_litter;
+  st[ow + 4 * (size_t)n] = s.pm;
+  st[ow + 5 * (size_t)n] = s.pfm;
+  st[ow + 6 * (size_t)n] = s.plen;
+  st[ow + 7 * (size_t)n] = s.rdepth;
   if (code) {
-    a.err[0 * (size_t)n + cw] = code;
-    a.err[1 * (size_t)n + cw] = eday;
-    a.err[2 * (size_t)n + cw] = estep;
-    a.err[3 * (size_t)n + cw] = __builtin_bit_cast(int, errval);
+    err[0 * (size_t)n + cw] = code;
+    err[1 * (size_t)n + cw] = eday;
+    err[2 * (size_t)n + cw] = estep;
+    err[3 * (size_t)n + cw] = __builtin_bit_cast(int, errval);
     atomicOr(a.err_flag, 1);
 #pragma unroll
-    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + iow] = __builtin_nanf("");
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * ios + iow] = __builtin_nanf("");
   }
 }
 
@@ -316,6 +339,7 @@ h9g_solo_kernel(const KArgs a, const G g) {
   const int c = a.perm ? a.perm[slot] : slot;
   const int io = a.sorted_io ? slot : c;
   const int n = a.ncell;
+  const size_t ios = a.sorted_io ? a.iostride : (size_t)n;
   SS cs{(lds_float *)&s_cell[threadIdx.x], (const lds_float *)s_zt};
   const SplitAll sp;
   St<L> s;
@@ -345,15 +369,15 @@ h9g_solo_kernel(const KArgs a, const G g) {
   for (int i = 1; i <= L; i++) ts_sum = ts_sum + cs.lay(PF_TS, i);
   if (!(ts_sum > 1.0E-8f) || a.err[c] != 0) {
 #pragma unroll
-    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + io] = __builtin_nanf("");
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * ios + io] = __builtin_nanf("");
     return;
   }
   cell_inv_pair<L, G>(g, cs);
   int eday = 0, estep = 0;
   float errval = 0.0f;
-  const int code = cell_year_pair<L, G, SplitAll, SS, false>(g, cs, sp, s, (const gbl_float *)(a.forc + io), (size_t)n, a.fvar,
+  const int code = cell_year_pair<L, G, SplitAll, SS, false>(g, cs, sp, s, (const gbl_float *)(a.forc + io), ios, a.fvar,
                                                              a.nt, a.nisurf, a.grow_on, (gbl_float *)(a.annual + io),
-                                                             (size_t)n, eday, estep, errval, T);
+                                                             ios, eday, estep, errval, T);
   int cw = c, iow = io;
   opaque(cw);
   opaque(iow);
@@ -382,7 +406,7 @@ h9g_solo_kernel(const KArgs a, const G g) {
     a.err[3 * (size_t)n + cw] = __builtin_bit_cast(int, errval);
     atomicOr(a.err_flag, 1);
 #pragma unroll
-    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * n + iow] = __builtin_nanf("");
+    for (int r = 0; r < 12 + L; r++) a.annual[(size_t)r * ios + iow] = __builtin_nanf("");
   }
 }
 
@@ -398,8 +422,10 @@ h9g_solo_kernel(const KArgs a, const G g) {
 // rows of one workgroup of XCD L % 8 -- so it reads only cells of its own
 // XCD's range, which the sort never leaves.
 #define H9G_PF_ROWS 32
+// Source rows have stride n (a forcing slot, variables fvar apart); the
+// slot-ordered copy has stride ds (variables dvar apart).
 __global__ void __launch_bounds__(256) h9g_perm_forcing_kernel(int c0, int cend, int cpb, int nt, int n, size_t fvar,
-                                                               const int *__restrict__ perm,
+                                                               size_t ds, size_t dvar, const int *__restrict__ perm,
                                                                const float *__restrict__ src, float *__restrict__ dst) {
   const unsigned nb = (unsigned)((cend - c0 + cpb - 1) / cpb), x = blockIdx.x % H9G_NXCD, j = blockIdx.x / H9G_NXCD;
   const unsigned q = nb / H9G_NXCD, r = nb % H9G_NXCD, cnt = q + (x < r ? 1u : 0u);
@@ -410,8 +436,8 @@ __global__ void __launch_bounds__(256) h9g_perm_forcing_kernel(int c0, int cend,
     const int s = c0 + (int)(v * (unsigned)cpb + t % (unsigned)cpb);
     const unsigned row = r0 + t / (unsigned)cpb;
     if (s >= cend || row >= rows) continue;
-    const size_t off = (size_t)(row / (unsigned)nt) * fvar + (size_t)(row % (unsigned)nt) * n;
-    dst[off + s] = src[off + perm[s]];
+    const size_t v = row / (unsigned)nt, d = row % (unsigned)nt;
+    dst[v * dvar + d * ds + s] = src[v * fvar + d * (size_t)n + perm[s]];
   }
 }
 static unsigned perm_forcing_blocks(int c0, int cend, int cpb, int nt) {
@@ -420,14 +446,15 @@ static unsigned perm_forcing_blocks(int c0, int cend, int cpb, int nt) {
   return H9G_NXCD * cmax * ((7u * (unsigned)nt + H9G_PF_ROWS - 1) / H9G_PF_ROWS);
 }
 
-// The annual sums of a sorted year kernel (slot order) back to cell order:
-// the m slots of the launch, rows of stride n.
-__global__ void __launch_bounds__(256) h9g_unperm_annual_kernel(int m, int n, int rows, const int *__restrict__ perm,
+// The annual sums of a sorted year kernel (slot order, rows of stride ss)
+// back to cell order (rows of stride n): the m slots from s0 of the launch.
+__global__ void __launch_bounds__(256) h9g_unperm_annual_kernel(int m, int n, int rows, int s0, size_t ss,
+                                                                const int *__restrict__ perm,
                                                                 const float *__restrict__ src, float *__restrict__ dst) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= m) return;
+  const int s = s0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (s >= s0 + m) return;
   const int c = perm[s];
-  for (int r = blockIdx.y; r < rows; r += gridDim.y) dst[(size_t)r * n + c] = src[(size_t)r * n + s];
+  for (int r = blockIdx.y; r < rows; r += gridDim.y) dst[(size_t)r * n + c] = src[(size_t)r * ss + s];
 }
 
 // Cell-order mode (h9g_run_decade_ordered).  The reference's cell loop
@@ -439,23 +466,62 @@ __global__ void __launch_bounds__(256) h9g_unperm_annual_kernel(int m, int n, in
 // (first[j]), from what the chain's last cell pred[j] held when the decade
 // started.  h9g_chain_kernel compares that with the smp the cell last
 // started from (guess, L rows of n), takes it over where it differs and
-// flags the cell for a re-run.
+// flags the cell for a re-run.  st: every cell's state at the decade's end
+// as known now.  dirty (may be null): cells whose decade start changed after
+// the first pass ran (h9g_settle_kernel), flagged whatever their input.
 __global__ void __launch_bounds__(256) h9g_chain_kernel(int m, int n, int L, const int *__restrict__ chain,
                                                         const int *__restrict__ pred, const int *__restrict__ first,
                                                         const float *__restrict__ st, const float *__restrict__ st0,
-                                                        float *__restrict__ guess, int *__restrict__ flag) {
+                                                        float *__restrict__ guess, const int *__restrict__ dirty,
+                                                        int *__restrict__ flag) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
   const int k = chain[j];
   const float *src = first[j] ? st0 : st;
   const int p = pred[j];
-  int differ = 0;
+  int differ = dirty ? dirty[k] : 0;
   for (int i = 0; i < L; i++) {
     const float v = src[(size_t)(2 * L + i) * n + p];
     differ |= __float_as_uint(v) != __float_as_uint(guess[(size_t)i * n + k]);
     guess[(size_t)i * n + k] = v;
   }
   flag[j] = differ;
+}
+
+// Pipelined decades (h9g_run_ordered): decade D+1's first pass starts from
+// every cell's state as known when decade D's first pass and year-1 re-run
+// are done (st0); the cells D's later re-runs still change get their final
+// D end state (fin, fin_err) here once D has settled, and are marked dirty.
+// A dirty cell that has now STOPped (err0 != 0) leaves D+1: its state and
+// STOP record go back into the context (st, err) and D+1's last-year
+// checkpoint, and its annual means of D+1 (ny years of rows x n) are NaN.
+__global__ void __launch_bounds__(256) h9g_settle_kernel(int n, int srows, int rows, int ny,
+                                                         const float *__restrict__ fin, const int *__restrict__ fin_err,
+                                                         float *__restrict__ st0, int *__restrict__ err0,
+                                                         int *__restrict__ dirty, float *__restrict__ st,
+                                                         int *__restrict__ err, float *__restrict__ ck_last,
+                                                         int *__restrict__ eck_last, float *__restrict__ ann) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  bool same = true;
+  for (int r = 0; r < srows; r++)
+    same &= __float_as_uint(fin[(size_t)r * n + c]) == __float_as_uint(st0[(size_t)r * n + c]);
+  for (int r = 0; r < 4; r++) same &= fin_err[(size_t)r * n + c] == err0[(size_t)r * n + c];
+  if (same) return;
+  for (int r = 0; r < srows; r++) st0[(size_t)r * n + c] = fin[(size_t)r * n + c];
+  for (int r = 0; r < 4; r++) err0[(size_t)r * n + c] = fin_err[(size_t)r * n + c];
+  dirty[c] = 1;
+  if (err0[c] == 0) return;
+  for (int r = 0; r < srows; r++) {
+    st[(size_t)r * n + c] = st0[(size_t)r * n + c];
+    ck_last[(size_t)r * n + c] = st0[(size_t)r * n + c];
+  }
+  for (int r = 0; r < 4; r++) {
+    err[(size_t)r * n + c] = err0[(size_t)r * n + c];
+    eck_last[(size_t)r * n + c] = err0[(size_t)r * n + c];
+  }
+  for (int y = 0; y < ny; y++)
+    for (int r = 0; r < rows; r++) ann[((size_t)y * rows + r) * n + c] = __builtin_nanf("");
 }
 
 // Pass 0's input of every chain's first cell: the smp its chain's last cell
@@ -1013,7 +1079,17 @@ struct h9g_ctx {
   int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel, 3: both, 4: h9g_pair2_kernel (L = 10)
                        // (H9G_KERNEL=pair|solo|mixed|pair2; default by L and the shard size, l10_kind)
   size_t n_solo = 0;   // kind 3: cells [0, n_solo) run on the solo kernel, the rest on the pair kernel
+  size_t ios = 0;      // slots of the slot-ordered buffers (d_perm, d_forc_s, d_ann_s): the cells + H9G_G2_MAX
+  size_t stamp_words = 0;
+  int ev_kind[NEVT] = {};         // kernel kind and cell-years of each timed launch
+  int64_t ev_cells[NEVT] = {};
+  double kstat[8][3] = {};        // per kernel kind: launches, cell-years, ms (h9g_launch_stats)
+  struct OrdBufs *ord = nullptr;  // h9g_run_ordered's decade buffers
+  int64_t ord_stats[6] = {};      // last ordered call (h9g_ordered_stats)
+  std::vector<int64_t> ord_passes;
 };
+
+static void ord_free(h9g_ctx *ctx);
 
 #define HIPCHK(x)                                                              \
   do {                                                                         \
@@ -1153,6 +1229,7 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_hist);
   (void)hipFree(ctx->d_aqbits);
   (void)hipFree(ctx->d_pace);
+  ord_free(ctx);
   for (auto e : ctx->ev_copied) hipEventDestroy(e);
   for (auto e : ctx->ev_consumed) hipEventDestroy(e);
   for (int i = 0; i < NEVT; i++) {
@@ -1196,17 +1273,31 @@ static int l10_kind(size_t n, int ncu, size_t *n_solo) {
 // arrays plus what the first h9g_run_year / h9g_soil_layer allocate lazily
 // (the pair kernel's per-workgroup day-snapshot blocks, the pacing rows, the
 // soil build's slow-cell flags).
+// Device bytes of the ordered mode's buffers for decades of up to ny years
+// (h9g_config_bytes counts them with ny = 10).
+static size_t ord_bytes(size_t n, size_t L, size_t ny) {
+  const size_t srows = 4 * L + 9, rows = 12 + L;
+  return 2 * (sizeof(float) * (srows + L + ny * (rows + srows)) * n + sizeof(int) * (4 + 4 * ny + 1) * n +
+              sizeof(int) * 5 * (n + 1)) +
+         sizeof(float) * srows * n + sizeof(int) * 4 * n;
+}
+
 size_t h9g_config_bytes(const h9g_config *cfg) {
   if (!cfg || cfg->ncell <= 0 || cfg->nlayers < 1 || cfg->max_days < 1 || cfg->nslots < 1) return 0;
   const size_t n = (size_t)cfg->ncell, L = (size_t)cfg->nlayers;
-  const size_t per_block = (size_t)H9G_PCPW11 * H9G_PWAVES;   // (the smallest workgroup: kind 5)
+  const size_t ios = round_up(n, H9G_PCPW) + H9G_G2_MAX;
+  // the largest launch's day-snapshot blocks: the 11-column kernel's over
+  // every cell, or the one-column kernel's over H9G_PAIR1_MAX listed cells
+  const size_t blocks = std::max((ios + (size_t)H9G_PCPW11 * H9G_PWAVES - 1) / ((size_t)H9G_PCPW11 * H9G_PWAVES),
+                                 (size_t)1024 / H9G_PWAVES);
   // + the slot-ordered copies of a forcing slot and of the annual sums
-  // (h9g_run_year, allocated on first use)
-  return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * ((size_t)cfg->nslots + 1) +
-                          2 * (12 + L) + 1) * n +
-         sizeof(int) * 7 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
-         ((n + per_block - 1) / per_block) * PairStore<8, H9G_PLANES>::GBLOCK +
-         sizeof(unsigned) * 16 * (size_t)H9G_PACE_ROWS;
+  // (h9g_run_year, allocated on first use), the ordered mode's decade
+  // buffers (h9g_run_ordered, decades of up to 10 years)
+  return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * (size_t)cfg->nslots + (12 + L) + 1) * n +
+         sizeof(float) * (7 * (size_t)cfg->max_days + 12 + L) * ios + sizeof(int) * ios +
+         sizeof(int) * 6 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
+         blocks * PairStore<8, H9G_PLANES>::GBLOCK + sizeof(unsigned) * 16 * (size_t)H9G_PACE_ROWS +
+         ord_bytes(n, L, 10);
 }
 
 // Free HBM h9g_create leaves beyond h9g_config_bytes (HIP runtime, RCCL
@@ -1267,6 +1358,7 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
   ctx->n = (size_t)cfg->ncell;
   const size_t n = ctx->n;
   const int L = ctx->L;
+  ctx->ios = round_up(n, H9G_PCPW) + H9G_G2_MAX;
   bool ok = hipStreamCreateWithFlags(&ctx->sc, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&ctx->sx, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&ctx->d_par, sizeof(float) * (4 * L + 1) * n) == hipSuccess &&
@@ -1278,7 +1370,7 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
             hipMalloc(&ctx->d_diag, sizeof(double) * H9G_NDIAG) == hipSuccess &&
             hipMalloc(&ctx->d_gid, sizeof(int64_t) * n) == hipSuccess &&
             hipMalloc(&ctx->d_lat, sizeof(float) * n) == hipSuccess &&
-            hipMalloc(&ctx->d_perm, sizeof(int) * n) == hipSuccess &&
+            hipMalloc(&ctx->d_perm, sizeof(int) * ctx->ios) == hipSuccess &&
             hipMalloc(&ctx->d_hist, sizeof(int) * n) == hipSuccess;
   if (ok) {
     ok = hipMemset(ctx->d_err, 0, sizeof(int) * 4 * n) == hipSuccess &&
@@ -1519,80 +1611,145 @@ static int join_prefetch(h9g_ctx *ctx, int slot) {
   return rc;
 }
 
-// Cells per workgroup of a pair-kernel kind: 4 waves of 22 columns, or of 11
-// (kind 5, h9g_pair11_kernel).
-static size_t pair_block_cells(int kind) {
-  return (size_t)(kind == 5 ? H9G_PCPW11 : (kind == 6 ? 1 : H9G_PCPW)) * H9G_PWAVES;
-}
+// Columns per wave of a pair-kernel kind: 22, 11 (kind 5, h9g_pair11_kernel)
+// or 1 (kind 6, h9g_pair1_kernel); 4 waves per workgroup.
+static int pair_wave_cols(int kind) { return kind == 5 ? H9G_PCPW11 : (kind == 6 ? 1 : H9G_PCPW); }
+static size_t pair_block_cells(int kind) { return (size_t)pair_wave_cols(kind) * H9G_PWAVES; }
+// Workgroups of a pair-kernel kind resident per CU (= waves per SIMD).
+static int pair_kind_resident(int kind) { return kind == 4 ? 2 : (kind == 6 ? 1 : pair_resident<8>()); }
 // Lists of at most this many cells (the cell-order re-runs' tails) run on
 // h9g_pair1_kernel: every workgroup resident at one wave per SIMD.
 #define H9G_PAIR1_MAX 1024
-
-// Pacer mode of a pair launch over m cells (h9g_pair.h Pacer): pace when all
-// its workgroups are resident at once (one round), else rotate -- a wave of a
-// later round starts hundreds of days behind the waves it shares a SIMD with.
-static int pace_mode(const h9g_ctx *ctx, size_t m) {
+// Pacer mode of a pair launch of `blocks` workgroups (h9g_pair.h Pacer): pace
+// when all of them are resident at once (one round), else rotate -- a wave of
+// a later round starts hundreds of days behind the waves it shares a SIMD with.
+static int pace_mode(const h9g_ctx *ctx, int kind, size_t blocks) {
   if (ctx->prio_mode >= 0) return ctx->prio_mode;
-  const size_t per_block = pair_block_cells(ctx->kind);
-  const size_t blocks = (m + per_block - 1) / per_block;
-  const int resident = ctx->kind == 4 ? 2 : (ctx->kind == 5 ? 3 : (ctx->L <= 8 ? pair_resident<8>() : pair_resident<10>()));
-  return blocks <= (size_t)ctx->ncu * resident ? 2 : 1;
+  return blocks <= (size_t)ctx->ncu * pair_kind_resident(kind) ? 2 : 1;
 }
 
-// One year launch.  d_list == nullptr: every cell of the context, in the
-// order of h9g_sort_kernel (h9g_run_year).  Otherwise the m cells d_list[0..m)
-// in that order (the cell-order mode's re-runs, h9g_run_decade_ordered),
-// their annual means to ann_dst (rows of stride n, cell order).
-static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, int m, float *ann_dst) {
-  if (!ctx || slot < 0 || slot >= ctx->cfg.nslots || jyear < 1861 || jyear > 2299) return H9G_EINVAL;
+// Whether an every-cell launch can carry k more cells in a second group for
+// free: a pair kernel kind, and the extra waves fit the launch's last round
+// of resident workgroups.
+static bool g2_fits(const h9g_ctx *ctx, size_t k) {
+  if (k == 0 || k > H9G_G2_MAX || !ctx->sort || !(ctx->kind == 1 || ctx->kind == 4 || ctx->kind == 5)) return false;
+#if defined(H9G_DUMP_AQ)
+  return false;
+#endif
+  const size_t C = (size_t)pair_wave_cols(ctx->kind), per = pair_block_cells(ctx->kind);
+  const size_t slots = (size_t)ctx->ncu * pair_kind_resident(ctx->kind);
+  const size_t b1 = (ctx->n + per - 1) / per, b2 = (round_up(ctx->n, C) + k + per - 1) / per;
+  return (b2 + slots - 1) / slots == (b1 + slots - 1) / slots;
+}
+
+// Fold the finished launches' HIP-event timings into the totals and the
+// per-kernel-kind counts (synchronises the compute stream).
+static int fold_events(h9g_ctx *ctx) {
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  for (int i = 0; i < ctx->nev; i++) {
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0[i], ctx->ev1[i]));
+    ctx->total_ms += ms;
+    ctx->last_ms = ms;
+    const int k = ctx->ev_kind[i];
+    ctx->kstat[k][0] += 1.0;
+    ctx->kstat[k][1] += (double)ctx->ev_cells[i];
+    ctx->kstat[k][2] += ms;
+  }
+  ctx->nev = 0;
+  return 0;
+}
+
+// One year launch (run_year_impl).
+struct YearSpec {
+  int slot = 0, jyear = 0;
+  const int *d_list = nullptr;   // null: every cell, in h9g_sort_kernel's order; else the m cells d_list[0..m)
+  int m = 0;
+  float *ann_dst = nullptr;      // list launches: their annual means into these rows (stride n, cell order)
+  float *st = nullptr;           // the cells' state and STOP rows (null: the context's own)
+  int *err = nullptr;
+  // every-cell launches of a pair kernel (g2_fits): a second group of the k2
+  // cells h2[0..k2) (host) at year jyear2 from slot2, with state st2/err2,
+  // annual means into ann2 (h9g_run_ordered: a decade's re-runs riding in the
+  // next decade's years)
+  const int *h2 = nullptr;
+  int k2 = 0, slot2 = 0, jyear2 = 0;
+  float *st2 = nullptr, *ann2 = nullptr;
+  int *err2 = nullptr;
+};
+
+static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
+  const int *d_list = ys.d_list;
+  const int m = ys.m;
+  if (!ctx || ys.slot < 0 || ys.slot >= ctx->cfg.nslots || ys.jyear < 1861 || ys.jyear > 2299) return H9G_EINVAL;
+  if (d_list && (m < 1 || (size_t)m > ctx->n || !ys.ann_dst)) return H9G_EINVAL;
+  const bool two = ys.k2 > 0;
+  if (two && (d_list || !ys.h2 || !ys.st2 || !ys.err2 || !ys.ann2 || ys.slot2 < 0 || ys.slot2 >= ctx->cfg.nslots ||
+              ys.jyear2 < 1861 || ys.jyear2 > 2299 || !g2_fits(ctx, (size_t)ys.k2)))
+    return H9G_EINVAL;
   if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
 #if defined(H9G_DUMP_AQ)
-  if (d_list) return H9G_EINVAL;
+  if (d_list || ys.st) return H9G_EINVAL;   // (the record is indexed by the annual array's cell)
 #endif
-  if (const int prc = join_prefetch(ctx, slot)) return prc;
-  const int nt = days_in_year(jyear);
-  if (ctx->slot_days[slot] < nt) return H9G_EINVAL;
+  if (const int prc = join_prefetch(ctx, ys.slot)) return prc;
+  if (two)
+    if (const int prc = join_prefetch(ctx, ys.slot2)) return prc;
+  const int nt = days_in_year(ys.jyear), nt2 = two ? days_in_year(ys.jyear2) : nt;
+  if (ctx->slot_days[ys.slot] < nt || (two && ctx->slot_days[ys.slot2] < nt2)) return H9G_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
-  HIPCHK(hipStreamWaitEvent(ctx->sc, ctx->ev_copied[slot], 0));
+  HIPCHK(hipStreamWaitEvent(ctx->sc, ctx->ev_copied[ys.slot], 0));
+  if (two) HIPCHK(hipStreamWaitEvent(ctx->sc, ctx->ev_copied[ys.slot2], 0));
+  const int n = (int)ctx->n;
+  const size_t ios = ctx->ios;
   KArgs a;
-  a.ncell = (int)ctx->n;
+  a.ncell = n;
   a.c0 = 0;
-  a.cend = d_list ? m : (int)ctx->n;
+  a.cend = d_list ? m : n;
   a.nt = nt;
   a.nisurf = ctx->cfg.nisurf;
   a.grow_on = ctx->cfg.grow_on;
   a.fvar = (size_t)ctx->cfg.max_days * ctx->n;
   a.par = ctx->d_par;
-  a.st = ctx->d_st;
-  a.forc = h9g_forcing_slot(ctx, slot);
+  a.st = ys.st ? ys.st : ctx->d_st;
+  a.forc = h9g_forcing_slot(ctx, ys.slot);
   a.annual = ctx->d_ann;
-  a.err = ctx->d_err;
+  a.err = ys.err ? ys.err : ctx->d_err;
   a.err_flag = ctx->d_errflag;
   a.stamps = nullptr;
   a.sv = nullptr;
   a.perm = nullptr;
   a.sorted_io = 0;
-  a.hist = ctx->d_hist;
+  a.hist = ys.st ? nullptr : ctx->d_hist;   // sort history: the context's own cells only
+  a.bend = a.split = a.cend;
+  a.nt2 = nt;
+  a.st2 = a.st;
+  a.err2 = a.err;
+  a.iostride = ios;
   // the launch's kernel: a list runs on the pair kernel (or the one the
-  // context's shard size chose at L = 10), never split into solo rounds
+  // context's shard size chose at L = 10), never split into solo rounds;
   // short lists (the cell-order re-runs' tails) on the one-column kernel
   const int kind = d_list ? (m <= H9G_PAIR1_MAX && ctx->kind != 2 && !getenv("H9G_NO_PAIR1") ? 6
                                                                                : (ctx->kind == 3 ? 1 : ctx->kind))
                           : ctx->kind;
   const size_t ncells = d_list ? (size_t)m : ctx->n;
+  // slot-ordered forcing and annual sums (row stride ios: the cells plus a
+  // second group's slack)
+  if (d_list || ctx->sort) {
+    if (!ctx->d_forc_s) HIPCHK(hipMalloc(&ctx->d_forc_s, sizeof(float) * 7 * (size_t)ctx->cfg.max_days * ios));
+    if (!ctx->d_ann_s) HIPCHK(hipMalloc(&ctx->d_ann_s, sizeof(float) * (12 + ctx->L) * ios));
+  }
+  const size_t dvar = (size_t)ctx->cfg.max_days * ios;
   if (d_list) {
     const int pcpb = kind == 2 ? H9G_YBLOCK : (int)pair_block_cells(kind);
-    if (!ctx->d_forc_s) HIPCHK(hipMalloc(&ctx->d_forc_s, sizeof(float) * 7 * (size_t)ctx->cfg.max_days * ctx->n));
-    if (!ctx->d_ann_s) HIPCHK(hipMalloc(&ctx->d_ann_s, sizeof(float) * (12 + ctx->L) * ctx->n));
     a.perm = d_list;
     h9g_perm_forcing_kernel<<<perm_forcing_blocks(0, m, pcpb, nt), 256, 0, ctx->sc>>>(
-        0, m, pcpb, nt, (int)ctx->n, a.fvar, d_list, a.forc, ctx->d_forc_s);
+        0, m, pcpb, nt, n, a.fvar, ios, dvar, d_list, a.forc, ctx->d_forc_s);
     HIPCHK(hipGetLastError());
     a.forc = ctx->d_forc_s;
     a.annual = ctx->d_ann_s;
     a.sorted_io = 1;
   } else if (ctx->sort) {             // per launch range and its workgroup size (h9g_sort_kernel)
-    const int n = (int)ctx->n, ns = (int)ctx->n_solo, pcpb = (int)pair_block_cells(ctx->kind);
+    const int ns = (int)ctx->n_solo, pcpb = (int)pair_block_cells(ctx->kind);
     if (ctx->kind == 2) {
       H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, n, H9G_YBLOCK, ctx->d_st, ctx->d_err,
                    ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
@@ -1610,21 +1767,31 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
     HIPCHK(hipGetLastError());
     a.perm = ctx->d_perm;
 #if !defined(H9G_DUMP_AQ)                 // (that record is indexed by the annual array's cell)
-    // forcing and annual sums in slot order for the year kernel
-    if (!ctx->d_forc_s) HIPCHK(hipMalloc(&ctx->d_forc_s, sizeof(float) * 7 * (size_t)ctx->cfg.max_days * ctx->n));
-    if (!ctx->d_ann_s) HIPCHK(hipMalloc(&ctx->d_ann_s, sizeof(float) * (12 + ctx->L) * ctx->n));
-    // per launch range with its workgroup size, as the sort above
-    auto perm_range = [&](int c0, int cend, int cpb) {
-      h9g_perm_forcing_kernel<<<perm_forcing_blocks(c0, cend, cpb, nt), 256, 0, ctx->sc>>>(
-          c0, cend, cpb, nt, n, a.fvar, ctx->d_perm, a.forc, ctx->d_forc_s);
+    // forcing and annual sums in slot order for the year kernel, per launch
+    // range with its workgroup size, as the sort above
+    auto perm_range = [&](int c0, int cend, int cpb, int ntr, const float *src) {
+      h9g_perm_forcing_kernel<<<perm_forcing_blocks(c0, cend, cpb, ntr), 256, 0, ctx->sc>>>(
+          c0, cend, cpb, ntr, n, a.fvar, ios, dvar, ctx->d_perm, src, ctx->d_forc_s);
     };
     if (ctx->kind == 2) {
-      perm_range(0, n, H9G_YBLOCK);
+      perm_range(0, n, H9G_YBLOCK, nt, a.forc);
     } else if (ctx->kind == 3) {
-      if (ns > 0) perm_range(0, ns, H9G_YBLOCK);
-      if (ns < n) perm_range(ns, n, pcpb);
+      if (ns > 0) perm_range(0, ns, H9G_YBLOCK, nt, a.forc);
+      if (ns < n) perm_range(ns, n, pcpb, nt, a.forc);
     } else {
-      perm_range(0, n, pcpb);
+      perm_range(0, n, pcpb, nt, a.forc);
+    }
+    if (two) {
+      // the second group from the first whole wave after the cells: its slots
+      // of d_perm, then its year's forcing into them
+      const int split = (int)round_up(ctx->n, (size_t)pair_wave_cols(kind));
+      HIPCHK(hipMemcpyAsync(ctx->d_perm + split, ys.h2, sizeof(int) * ys.k2, hipMemcpyHostToDevice, ctx->sc));
+      perm_range(split, split + ys.k2, pcpb, nt2, h9g_forcing_slot(ctx, ys.slot2));
+      a.split = split;
+      a.cend = split + ys.k2;
+      a.nt2 = nt2;
+      a.st2 = ys.st2;
+      a.err2 = ys.err2;
     }
     HIPCHK(hipGetLastError());
     a.forc = ctx->d_forc_s;
@@ -1632,9 +1799,14 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
     a.sorted_io = 1;
 #endif
   }
+  if (a.sorted_io) a.fvar = dvar;
+  // workgroups of the launch (the pair part's, for the mixed kind)
+  const size_t per_block = kind == 2 ? (size_t)H9G_YBLOCK : pair_block_cells(kind == 3 ? 1 : kind);
+  const size_t blocks = kind == 3 ? (ctx->n - ctx->n_solo + per_block - 1) / per_block
+                                  : ((size_t)a.cend + per_block - 1) / per_block;
   if (kind != 2) {
-    const size_t per_block = pair_block_cells(kind);
-    const size_t need = ((ctx->n + per_block - 1) / per_block) * PairStore<8, H9G_PLANES>::GBLOCK;
+    // the pair kernels' day-snapshot blocks, one per workgroup of the launch
+    const size_t need = std::max<size_t>(blocks, 1) * PairStore<8, H9G_PLANES>::GBLOCK;
     if (ctx->sv_bytes < need) {
       (void)hipFree(ctx->d_sv);
       ctx->d_sv = nullptr;
@@ -1651,22 +1823,22 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
   }
   a.pace = ctx->d_pace;
   a.epoch = ++ctx->epoch;
-  a.prio_mode = pace_mode(ctx, kind == 3 ? ctx->n - ctx->n_solo : ncells);
+  a.prio_mode = pace_mode(ctx, kind == 3 ? 1 : kind, blocks);
 #if defined(H9G_STAMPS)
-  if (!ctx->d_stamps) HIPCHK(hipMalloc(&ctx->d_stamps, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8)));
-  HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, sizeof(unsigned) * 8 * (ctx->n / H9G_PCPW + 8), ctx->sc));
-  a.stamps = ctx->d_stamps;
-#endif
-  if (ctx->nev >= NEVT) {   // fold finished timings before reusing events
-    HIPCHK(hipStreamSynchronize(ctx->sc));
-    for (int i = 0; i < ctx->nev; i++) {
-      float ms = 0.0f;
-      (void)hipEventElapsedTime(&ms, ctx->ev0[i], ctx->ev1[i]);
-      ctx->total_ms += ms;
-      ctx->last_ms = ms;
+  {  // one record of 8 words per wave of the launch
+    const size_t words = (size_t)8 * H9G_PWAVES * (blocks + 1);
+    if (ctx->stamp_words < words) {
+      (void)hipFree(ctx->d_stamps);
+      ctx->d_stamps = nullptr;
+      HIPCHK(hipMalloc(&ctx->d_stamps, sizeof(unsigned) * words));
+      ctx->stamp_words = words;
     }
-    ctx->nev = 0;
+    HIPCHK(hipMemsetAsync(ctx->d_stamps, 0, sizeof(unsigned) * words, ctx->sc));
+    a.stamps = ctx->d_stamps;
   }
+#endif
+  if (ctx->nev >= NEVT)   // fold finished timings before reusing events
+    if (int r = fold_events(ctx)) return r;
 #if defined(H9G_DUMP_AQ)
   // the last year's record to $H9G_AQ_DUMP: year, n, then n x 12 words
   if (const char *path = getenv("H9G_AQ_DUMP"); path && ctx->d_aqbits && ctx->ran) {
@@ -1691,290 +1863,493 @@ static int run_year_impl(h9g_ctx *ctx, int slot, int jyear, const int *d_list, i
   }
 #endif
   const int e = ctx->nev++;
+  ctx->ev_kind[e] = kind;
+  ctx->ev_cells[e] = (int64_t)ncells + (two ? ys.k2 : 0);
   HIPCHK(hipEventRecord(ctx->ev0[e], ctx->sc));
   if (kind == 2) {
     H9G_DISPATCH(ctx, h9g_solo_kernel, (unsigned)((ncells + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
                  ctx->sc, a);
   } else if (kind == 3) {
     // mixed (l10_kind): whole rounds of solo waves, then the pair kernel on the rest
-    const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
     const size_t ns = ctx->n_solo;
     if (ns > 0) {
       a.c0 = 0;
-      a.cend = (int)ns;
+      a.cend = a.bend = a.split = (int)ns;
       H9G_DISPATCH(ctx, h9g_solo_kernel, (unsigned)((ns + H9G_YBLOCK - 1) / H9G_YBLOCK), H9G_YBLOCK,
                    ctx->sc, a);
     }
     if (ns < ctx->n) {
       a.c0 = (int)ns;
-      a.cend = (int)ctx->n;
-      H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ctx->n - ns + per_block - 1) / per_block), 64 * H9G_PWAVES,
-                   ctx->sc, a);
+      a.cend = a.bend = a.split = (int)ctx->n;
+      H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)blocks, 64 * H9G_PWAVES, ctx->sc, a);
     }
   } else if (kind == 4) {
-    const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
-    H9G_DISPATCH_L10(ctx, h9g_pair2_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
-                     ctx->sc, a);
+    H9G_DISPATCH_L10(ctx, h9g_pair2_kernel, (unsigned)blocks, 64 * H9G_PWAVES, ctx->sc, a);
   } else if (kind == 5) {
-    const size_t per_block = pair_block_cells(5);
-    H9G_DISPATCH(ctx, h9g_pair11_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
-                 ctx->sc, a);
+    H9G_DISPATCH(ctx, h9g_pair11_kernel, (unsigned)blocks, 64 * H9G_PWAVES, ctx->sc, a);
   } else if (kind == 6) {
-    const size_t per_block = pair_block_cells(6);
-    H9G_DISPATCH(ctx, h9g_pair1_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
-                 ctx->sc, a);
+    H9G_DISPATCH(ctx, h9g_pair1_kernel, (unsigned)blocks, 64 * H9G_PWAVES, ctx->sc, a);
   } else {
-    const size_t per_block = (size_t)H9G_PCPW * H9G_PWAVES;
-    H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)((ncells + per_block - 1) / per_block), 64 * H9G_PWAVES,
-                 ctx->sc, a);
+    H9G_DISPATCH(ctx, h9g_pair_kernel, (unsigned)blocks, 64 * H9G_PWAVES, ctx->sc, a);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev1[e], ctx->sc));
-  HIPCHK(hipEventRecord(ctx->ev_consumed[slot], ctx->sc));
+  HIPCHK(hipEventRecord(ctx->ev_consumed[ys.slot], ctx->sc));
+  if (two) HIPCHK(hipEventRecord(ctx->ev_consumed[ys.slot2], ctx->sc));
   if (a.sorted_io) {
-    h9g_unperm_annual_kernel<<<dim3((unsigned)((ncells + 255) / 256), (unsigned)(12 + ctx->L)), 256, 0, ctx->sc>>>(
-        (int)ncells, (int)ctx->n, 12 + ctx->L, a.perm, ctx->d_ann_s, d_list ? ann_dst : ctx->d_ann);
+    const unsigned rows = (unsigned)(12 + ctx->L);
+    h9g_unperm_annual_kernel<<<dim3((unsigned)((ncells + 255) / 256), rows), 256, 0, ctx->sc>>>(
+        (int)ncells, n, (int)rows, 0, ios, a.perm, ctx->d_ann_s, d_list ? ys.ann_dst : ctx->d_ann);
+    if (two)
+      h9g_unperm_annual_kernel<<<dim3((unsigned)((ys.k2 + 255) / 256), rows), 256, 0, ctx->sc>>>(
+          ys.k2, n, (int)rows, a.split, ios, a.perm, ctx->d_ann_s, ys.ann2);
     HIPCHK(hipGetLastError());
   }
   if (!d_list) {
     h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)ctx->n, ctx->L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
     HIPCHK(hipGetLastError());
   }
-  ctx->last_year = jyear;
-  ctx->hist_nsub = nt * ctx->cfg.nisurf;
+  if (!ys.st) {
+    ctx->last_year = ys.jyear;
+    ctx->hist_nsub = nt * ctx->cfg.nisurf;
+  }
   ctx->ran = 1;
   return 0;
 }
 
-int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) { return run_year_impl(ctx, slot, jyear, nullptr, 0, nullptr); }
+int h9g_run_year(h9g_ctx *ctx, int slot, int jyear) {
+  YearSpec ys;
+  ys.slot = slot;
+  ys.jyear = jyear;
+  return run_year_impl(ctx, ys);
+}
 
-// The reference's own cell order over one decade (include/h9g.h).  Pass 0
-// runs every cell from its own smp, except the chain's first cell, whose
-// input is known.  Each further pass gives every land cell the smp its
-// predecessor now leaves behind (h9g_chain_kernel) and re-runs the decade
-// for the cells whose input changed, from the decade's starting state.  A
-// cell's result depends on its predecessor's only through that smp, so when
-// no input changes every cell has run from the input the reference gives
-// it.  The chain's first cell never changes after pass 0, so pass p fixes
-// at least chain position p: at most m passes.
+// ---------------------------------------------------------------------------
+// The reference's own cell order (h9g_run_ordered, h9g_run_decade_ordered)
+// ---------------------------------------------------------------------------
+// One decade of the reference's loop (HYBRID9.f90:93-130) is a fixed point
+// on the device.  Pass 0 runs every cell's years from its own smp.
+// h9g_chain_kernel then gives every land cell the smp its predecessor now
+// ends the decade with and flags the cells whose input changed; those
+// re-run from the decade's starting state (h9g_restart_kernel), and the pass
+// repeats until no input changes.  A cell's result depends on its
+// predecessor's only through that smp, so when no input changes every cell
+// has run from the input the reference gives it.  Position p of a chain is
+// exact after pass p + 1 at the latest: at most m + 1 passes.
 //
 // A re-run stops early.  The input smp reaches a cell's decade only through
 // beta of its first substep (HYDROLOGY.f90:270-275), and the perturbation
 // it starts is rounded away within months in most cells: from then on the
 // cell runs bit for bit as before.  Every run therefore checkpoints each
-// cell's state and STOP record at every year end (ckpt), and after each
+// cell's state and STOP record at every year end (ck), and after each
 // re-run year h9g_merge_kernel drops the cells whose state is the
 // checkpoint's again: they keep the old trajectory's later years and end
 // state (and so the input their successor already has).  Pass 1 then costs
-// about one year for most cells instead of ten (DESIGN.md §2).
-int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int nyears, float *annual, int32_t *passes) {
-  if (!ctx || !slots || nyears < 1 || nyears > ctx->cfg.nslots) return H9G_EINVAL;
-  if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
+// about one year for most cells instead of ten.
+//
+// Decades overlap (round 6).  Decade D+1's first pass needs only every
+// cell's own end state of D, which the first pass of D gives for every cell
+// the re-runs leave alone; so it starts as soon as D's first pass and the
+// re-run of year 1 (every cell whose input changed) are done.  D's
+// remaining re-runs -- a tail of a few dozen cells whose perturbation
+// lasts, run year by year -- ride as a second group of waves in D+1's year
+// launches (KArgs::split, on their own state rows st2), in the slots the
+// grid leaves free in the launch's last round of resident workgroups.  Once
+// D has settled, the cells whose end of D differs from where D+1's first
+// pass started them get their final state (h9g_settle_kernel) and are
+// re-run in D+1's first check whatever their input.  Each decade's first
+// pass, checkpoints and re-runs read only its own buffers (OrdDec), so D's
+// tail and D+1's first pass are independent.
+struct OrdDec {
+  int y0 = 0, ny = 0, k0 = 0;            // first year, years, index of its first year in the call
+  float *st0 = nullptr, *guess = nullptr, *ann = nullptr, *ck = nullptr;
+  int *err0 = nullptr, *eck = nullptr, *dirty = nullptr;
+  int *d_chain = nullptr, *d_pred = nullptr, *d_first = nullptr, *d_list = nullptr, *d_flag = nullptr;
+  std::vector<int> chain, list, flag;
+  int m = 0;
+  enum { PASS0, CHECK, RERUN, SETTLED } phase = PASS0;
+  int next_y = 0, np = 0;
+};
+
+struct OrdBufs {
+  OrdDec d[2];
+  float *st2 = nullptr;                  // the re-running cells' state and STOP rows
+  int *err2 = nullptr;
+  int ny_cap = 0;
+};
+
+static void ord_free(h9g_ctx *ctx) {
+  OrdBufs *o = ctx->ord;
+  if (!o) return;
+  for (OrdDec &D : o->d) {
+    for (float *p : {D.st0, D.guess, D.ann, D.ck}) (void)hipFree(p);
+    for (int *p : {D.err0, D.eck, D.dirty, D.d_chain, D.d_pred, D.d_first, D.d_list, D.d_flag}) (void)hipFree(p);
+  }
+  (void)hipFree(o->st2);
+  (void)hipFree(o->err2);
+  delete o;
+  ctx->ord = nullptr;
+}
+
+static int ord_alloc(h9g_ctx *ctx, int ny) {
+  if (ctx->ord && ctx->ord->ny_cap >= ny) return 0;
+  ord_free(ctx);
+  ctx->ord = new OrdBufs();
+  OrdBufs *o = ctx->ord;
+  const size_t n = ctx->n, L = (size_t)ctx->L, srows = (size_t)h9g_state_size(ctx->L), rows = 12 + L;
+  bool ok = hipMalloc(&o->st2, sizeof(float) * srows * n) == hipSuccess &&
+            hipMalloc(&o->err2, sizeof(int) * 4 * n) == hipSuccess;
+  for (OrdDec &D : o->d) {
+    ok = ok && hipMalloc(&D.st0, sizeof(float) * srows * n) == hipSuccess &&
+         hipMalloc(&D.guess, sizeof(float) * L * n) == hipSuccess &&
+         hipMalloc(&D.ann, sizeof(float) * (size_t)ny * rows * n) == hipSuccess &&
+         hipMalloc(&D.ck, sizeof(float) * (size_t)ny * srows * n) == hipSuccess &&
+         hipMalloc(&D.err0, sizeof(int) * 4 * n) == hipSuccess &&
+         hipMalloc(&D.eck, sizeof(int) * (size_t)ny * 4 * n) == hipSuccess &&
+         hipMalloc(&D.dirty, sizeof(int) * n) == hipSuccess;
+    for (int **p : {&D.d_chain, &D.d_pred, &D.d_first, &D.d_list, &D.d_flag})
+      ok = ok && hipMalloc(p, sizeof(int) * (n + 1)) == hipSuccess;
+  }
+  if (!ok) {
+    ord_free(ctx);
+    return H9G_ENOMEM;
+  }
+  o->ny_cap = ny;
+  return 0;
+}
+
+// Work counters of the last ordered call (h9g_decade_stats, h9g_ordered_stats).
+struct OrdStats {
+  int64_t passes = 0, rerun_cells = 0, rerun_cell_years = 0, rerun_launches = 0;
+  int64_t ticks = 0, ride_steps = 0, ride_cell_years = 0, alone_steps = 0, alone_cell_years = 0;
+  std::vector<int64_t> launch_cells, dec_passes;
+};
+
+static float *ord_ck(const h9g_ctx *ctx, const OrdDec &D, int y) {
+  return D.ck + (size_t)y * h9g_state_size(ctx->L) * ctx->n;
+}
+static int *ord_eck(const h9g_ctx *ctx, const OrdDec &D, int y) { return D.eck + (size_t)y * 4 * ctx->n; }
+static float *ord_ann(const h9g_ctx *ctx, const OrdDec &D, int y) { return D.ann + (size_t)y * (12 + ctx->L) * ctx->n; }
+
+// The decade's chains (h9g_set_chains) over its land cells that have not
+// stopped when it starts (its final err0), in context order: predecessors
+// are the previous land cell of the same chain, for a chain's first cell its
+// last one.
+static int ord_chain(h9g_ctx *ctx, OrdDec &D, const std::vector<char> &land) {
+  const size_t n = ctx->n;
+  std::vector<int> e0(n);
+  HIPCHK(hipStreamSynchronize(ctx->sc));   // (the compute stream is non-blocking: hipMemcpy does not wait for it)
+  HIPCHK(hipMemcpy(e0.data(), D.err0, sizeof(int) * n, hipMemcpyDeviceToHost));
+  D.chain.clear();
+  for (size_t c = 0; c < n; c++)
+    if (land[c] && e0[c] == 0) D.chain.push_back((int)c);
+  const int m = D.m = (int)D.chain.size();
+  std::vector<int> pred(m), first(m), last_of, first_of;
+  auto cid = [&](int j) { return ctx->chain_id.empty() ? 0 : ctx->chain_id[(size_t)D.chain[j]]; };
+  for (int j = 0; j < m; j++) {
+    const int c = cid(j);
+    if ((int)last_of.size() <= c) {
+      last_of.resize((size_t)c + 1, -1);
+      first_of.resize((size_t)c + 1, -1);
+    }
+    if (last_of[(size_t)c] < 0) {
+      first_of[(size_t)c] = j;
+      first[j] = 1;
+    } else {
+      pred[j] = D.chain[last_of[(size_t)c]];
+      first[j] = 0;
+    }
+    last_of[(size_t)c] = j;
+  }
+  for (int j = 0; j < m; j++)
+    if (first[j]) pred[j] = D.chain[last_of[(size_t)cid(j)]];
+  if (m > 0) {
+    HIPCHK(hipMemcpy(D.d_chain, D.chain.data(), sizeof(int) * m, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D.d_pred, pred.data(), sizeof(int) * m, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(D.d_first, first.data(), sizeof(int) * m, hipMemcpyHostToDevice));
+  }
+  D.flag.assign((size_t)m + 1, 0);
+  return 0;
+}
+
+// A check of decade D: every chain cell's input from its predecessor's end
+// of the decade as known now (the last year's checkpoint); the flagged cells
+// back to the decade's start on the re-run rows st2 (phase RERUN), or, with
+// none flagged, D has settled.
+static int ord_check(h9g_ctx *ctx, OrdDec &D, bool use_dirty, OrdStats &S) {
+  OrdBufs *o = ctx->ord;
+  const int n = (int)ctx->n, L = ctx->L, m = D.m;
+  D.list.clear();
+  if (m > 0) {
+    h9g_chain_kernel<<<(unsigned)((m + 255) / 256), 256, 0, ctx->sc>>>(m, n, L, D.d_chain, D.d_pred, D.d_first,
+                                                                      ord_ck(ctx, D, D.ny - 1), D.st0, D.guess,
+                                                                      use_dirty ? D.dirty : nullptr, D.d_flag);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(D.flag.data(), D.d_flag, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->sc));
+    HIPCHK(hipStreamSynchronize(ctx->sc));
+    for (int j = 0; j < m; j++)
+      if (D.flag[j]) D.list.push_back(D.chain[j]);
+  }
+  if (D.list.empty()) {
+    D.phase = OrdDec::SETTLED;
+    return 0;
+  }
+  if (D.np > m + 1) return H9G_ESTATE;   // cannot happen (see above): a broken invariant, not a result
+  const int k = (int)D.list.size();
+  HIPCHK(hipMemcpy(D.d_list, D.list.data(), sizeof(int) * k, hipMemcpyHostToDevice));
+  h9g_restart_kernel<<<(unsigned)((k + 255) / 256), 256, 0, ctx->sc>>>(k, n, L, D.d_list, D.st0, D.err0, D.guess,
+                                                                      o->st2, o->err2);
+  HIPCHK(hipGetLastError());
+  S.rerun_cells += k;
+  D.next_y = 0;
+  D.phase = OrdDec::RERUN;
+  return 0;
+}
+
+// After a re-run year of decade D's list: the cells back on their old
+// trajectory leave the re-run (h9g_merge_kernel); at the decade's end, or
+// with none left, the pass ends and a check follows.
+static int ord_after_run(h9g_ctx *ctx, OrdDec &D, OrdStats &S) {
+  OrdBufs *o = ctx->ord;
+  const int n = (int)ctx->n, srows = h9g_state_size(ctx->L);
+  const int k = (int)D.list.size(), y = D.next_y;
+  h9g_merge_kernel<<<(unsigned)((k + 255) / 256), 256, 0, ctx->sc>>>(k, n, srows, D.d_list, o->st2, o->err2,
+                                                                    ord_ck(ctx, D, y), ord_eck(ctx, D, y),
+                                                                    ord_ck(ctx, D, D.ny - 1), ord_eck(ctx, D, D.ny - 1),
+                                                                    D.d_flag);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(D.flag.data(), D.d_flag, sizeof(int) * k, hipMemcpyDeviceToHost, ctx->sc));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  S.rerun_cell_years += k;
+  S.rerun_launches++;
+  S.launch_cells.push_back(k);
+  int kk = 0;
+  for (int j = 0; j < k; j++)
+    if (D.flag[j]) D.list[kk++] = D.list[j];
+  D.list.resize(kk);
+  if (kk > 0 && kk < k) HIPCHK(hipMemcpy(D.d_list, D.list.data(), sizeof(int) * kk, hipMemcpyHostToDevice));
+  D.next_y = y + 1;
+  if (kk == 0 || D.next_y == D.ny) {
+    D.np++;
+    D.phase = OrdDec::CHECK;
+  }
+  return 0;
+}
+
+// One re-run year of decade D's list as a launch of its own.
+static int ord_run_alone(h9g_ctx *ctx, OrdDec &D, const int32_t *slots, OrdStats &S) {
+  YearSpec ys;
+  ys.slot = slots[D.k0 + D.next_y];
+  ys.jyear = D.y0 + D.next_y;
+  ys.d_list = D.d_list;
+  ys.m = (int)D.list.size();
+  ys.ann_dst = ord_ann(ctx, D, D.next_y);
+  ys.st = ctx->ord->st2;
+  ys.err = ctx->ord->err2;
+  if (int r = run_year_impl(ctx, ys)) return r;
+  S.alone_steps++;
+  S.alone_cell_years += ys.m;
+  return ord_after_run(ctx, D, S);
+}
+
+// Runs D's checks and re-runs until it has settled.
+static int ord_settle(h9g_ctx *ctx, OrdDec &D, const int32_t *slots, OrdStats &S) {
+  while (D.phase != OrdDec::SETTLED) {
+    const int r = D.phase == OrdDec::CHECK ? ord_check(ctx, D, false, S) : ord_run_alone(ctx, D, slots, S);
+    if (r) return r;
+  }
+  return 0;
+}
+
+// D has settled: its annual means to the host, its first new STOP into the
+// context's error record, and -- with a next decade N under way -- its end
+// states into N's start (h9g_settle_kernel).
+static int ord_finish(h9g_ctx *ctx, OrdDec &D, OrdDec *N, float *annual, int &stop_seen) {
+  const size_t n = ctx->n;
+  const int rows = 12 + ctx->L, srows = h9g_state_size(ctx->L);
+  if (annual)
+    HIPCHK(hipMemcpyAsync(annual + (size_t)D.k0 * rows * n, D.ann, sizeof(float) * (size_t)D.ny * rows * n,
+                          hipMemcpyDeviceToHost, ctx->sc));
+  if (!stop_seen && ctx->last_err.code == 0) {
+    std::vector<int> e0(n), e1(4 * n);
+    HIPCHK(hipMemcpyAsync(e0.data(), D.err0, sizeof(int) * n, hipMemcpyDeviceToHost, ctx->sc));
+    HIPCHK(hipMemcpyAsync(e1.data(), ord_eck(ctx, D, D.ny - 1), sizeof(int) * 4 * n, hipMemcpyDeviceToHost, ctx->sc));
+    HIPCHK(hipStreamSynchronize(ctx->sc));
+    for (size_t c = 0; c < n; c++) {
+      if (e1[c] == 0 || e0[c] != 0) continue;
+      // the first cell in context order to STOP in this decade, in the first
+      // year of the decade whose means it has not completed
+      std::vector<float> npp(D.ny);
+      for (int y = 0; y < D.ny; y++)
+        HIPCHK(hipMemcpy(&npp[y], ord_ann(ctx, D, y) + c, sizeof(float), hipMemcpyDeviceToHost));
+      int y = 0;
+      while (y < D.ny - 1 && npp[y] == npp[y]) y++;
+      ctx->last_err.code = e1[c];
+      ctx->last_err.cell = (int)c;
+      ctx->last_err.year = D.y0 + y;
+      ctx->last_err.day = e1[n + c];
+      ctx->last_err.substep = e1[2 * n + c];
+      ctx->last_err.value = __builtin_bit_cast(float, e1[3 * n + c]);
+      stop_seen = 1;
+      break;
+    }
+  }
+  if (N) {
+    h9g_settle_kernel<<<(unsigned)((n + 255) / 256), 256, 0, ctx->sc>>>(
+        (int)n, srows, rows, N->ny, ord_ck(ctx, D, D.ny - 1), ord_eck(ctx, D, D.ny - 1), N->st0, N->err0, N->dirty,
+        ctx->d_st, ctx->d_err, ord_ck(ctx, *N, N->ny - 1), ord_eck(ctx, *N, N->ny - 1), N->ann);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  return 0;
+}
+
+// decades: (first year, years) of each decade the call runs, in order;
+// their years' forcing in slots[0 .. sum of years).
+static int run_ordered_impl(h9g_ctx *ctx, const int32_t *slots, int jyear0,
+                            const std::vector<std::pair<int, int>> &decs, float *annual, int32_t *passes) {
+  if (!ctx || !slots || decs.empty()) return H9G_EINVAL;
+  int nyears = 0, nymax = 0;
+  for (auto &d : decs) {
+    nyears += d.second;
+    nymax = std::max(nymax, d.second);
+  }
+  if (nyears < 1 || nymax > ctx->cfg.nslots) return H9G_EINVAL;
   for (int y = 0; y < nyears; y++)
     if (slots[y] < 0 || slots[y] >= ctx->cfg.nslots || jyear0 + y < 1861 || jyear0 + y > 2299) return H9G_EINVAL;
+  if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
   const size_t n = ctx->n;
-  const int L = ctx->L, rows = 12 + L;
+  const int L = ctx->L, rows = 12 + L, srows = h9g_state_size(L);
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->sc));
-  // the chain: land cells (HYBRID9.f90:122-123, summed in layer order as the
-  // year kernels do) that have not stopped, in context order
-  std::vector<float> ts((size_t)L * n);
-  std::vector<int> err0h(n);
-  HIPCHK(hipMemcpy(ts.data(), ctx->d_par, sizeof(float) * ts.size(), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(err0h.data(), ctx->d_err, sizeof(int) * n, hipMemcpyDeviceToHost));
-  std::vector<int> chain;
-  for (size_t c = 0; c < n; c++) {
-    float sum = 0.0f;
-    for (int i = 0; i < L; i++) sum = sum + ts[(size_t)i * n + c];
-    if (sum > 1.0E-8f && err0h[c] == 0) chain.push_back((int)c);
-  }
-  const int m = (int)chain.size();
-  // predecessors: the previous land cell of the same chain (h9g_set_chains),
-  // for a chain's first cell its last one (read at the decade's start)
-  std::vector<int> pred(m), first(m);
+  if (int r = ord_alloc(ctx, nymax)) return r;
+  OrdBufs *o = ctx->ord;
+  // land cells (HYBRID9.f90:122-123, summed in layer order as the year
+  // kernels do)
+  std::vector<char> land(n);
   {
-    std::vector<int> last_of, first_of;   // per chain id: position of its last / first land cell
-    auto cid = [&](int j) { return ctx->chain_id.empty() ? 0 : ctx->chain_id[(size_t)chain[j]]; };
-    for (int j = 0; j < m; j++) {
-      const int c = cid(j);
-      if ((int)last_of.size() <= c) {
-        last_of.resize((size_t)c + 1, -1);
-        first_of.resize((size_t)c + 1, -1);
-      }
-      if (last_of[(size_t)c] < 0) {
-        first_of[(size_t)c] = j;
-        first[j] = 1;
-      } else {
-        pred[j] = chain[last_of[(size_t)c]];
-        first[j] = 0;
-      }
-      last_of[(size_t)c] = j;
-    }
-    for (int j = 0; j < m; j++)
-      if (first[j]) pred[j] = chain[last_of[(size_t)cid(j)]];
-  }
-  const size_t srows = (size_t)h9g_state_size(L);
-  float *d_st0 = nullptr, *d_guess = nullptr, *d_ann_dec = nullptr, *d_ck = nullptr;
-  int *d_err0 = nullptr, *d_chain = nullptr, *d_list = nullptr, *d_flag = nullptr, *d_eck = nullptr;
-  int *d_pred = nullptr, *d_first = nullptr;
-  int rc = 0, np = 0;
-  int64_t rerun_cells = 0, rerun_cell_years = 0, rerun_launches = 0;
-  std::vector<int64_t> launch_cells;   // cells of each re-run launch, in order
-  auto ck = [&](int y) { return d_ck + (size_t)y * srows * n; };
-  auto eck = [&](int y) { return d_eck + (size_t)y * 4 * n; };
-  auto fail = [&](int code) { rc = code; };
-  do {
-    if (hipMalloc(&d_st0, sizeof(float) * srows * n) != hipSuccess ||
-        hipMalloc(&d_guess, sizeof(float) * (size_t)L * n) != hipSuccess ||
-        hipMalloc(&d_ann_dec, sizeof(float) * (size_t)nyears * rows * n) != hipSuccess ||
-        hipMalloc(&d_err0, sizeof(int) * 4 * n) != hipSuccess || hipMalloc(&d_chain, sizeof(int) * (m + 1)) != hipSuccess ||
-        hipMalloc(&d_list, sizeof(int) * (m + 1)) != hipSuccess || hipMalloc(&d_flag, sizeof(int) * (m + 1)) != hipSuccess ||
-        hipMalloc(&d_pred, sizeof(int) * (m + 1)) != hipSuccess || hipMalloc(&d_first, sizeof(int) * (m + 1)) != hipSuccess ||
-        hipMalloc(&d_ck, sizeof(float) * (size_t)nyears * srows * n) != hipSuccess ||
-        hipMalloc(&d_eck, sizeof(int) * (size_t)nyears * 4 * n) != hipSuccess) {
-      fail(H9G_ENOMEM);
-      break;
-    }
-    if (hipMemcpyAsync(d_st0, ctx->d_st, sizeof(float) * srows * n, hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
-        hipMemcpyAsync(d_err0, ctx->d_err, sizeof(int) * 4 * n, hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
-        hipMemcpyAsync(d_guess, ctx->d_st + (size_t)2 * L * n, sizeof(float) * (size_t)L * n, hipMemcpyDeviceToDevice,
-                       ctx->sc) != hipSuccess) {
-      fail(H9G_EHIP);
-      break;
-    }
-    if (m > 0) {
-      if (hipMemcpy(d_chain, chain.data(), sizeof(int) * m, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(d_pred, pred.data(), sizeof(int) * m, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(d_first, first.data(), sizeof(int) * m, hipMemcpyHostToDevice) != hipSuccess) {
-        fail(H9G_EHIP);
-        break;
-      }
-      // pass 0's input of every chain's first cell: what its last one holds now
-      h9g_chain_start_kernel<<<(unsigned)((m + 255) / 256), 256, 0, ctx->sc>>>(m, (int)n, L, d_chain, d_pred, d_first,
-                                                                              d_st0, ctx->d_st, d_guess);
-      if (hipGetLastError() != hipSuccess) {
-        fail(H9G_EHIP);
-        break;
-      }
-    }
-    for (int y = 0; y < nyears && !rc; y++) {   // pass 0: every cell
-      if (int r = run_year_impl(ctx, slots[y], jyear0 + y, nullptr, 0, nullptr)) {
-        fail(r);
-        break;
-      }
-      if (hipMemcpyAsync(d_ann_dec + (size_t)y * rows * n, ctx->d_ann, sizeof(float) * rows * n,
-                         hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
-          hipMemcpyAsync(ck(y), ctx->d_st, sizeof(float) * srows * n, hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess ||
-          hipMemcpyAsync(eck(y), ctx->d_err, sizeof(int) * 4 * n, hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess)
-        fail(H9G_EHIP);
-    }
-    if (rc) break;
-    np = 1;
-    std::vector<int> flag(m), list;
-    while (m > 0) {
-      h9g_chain_kernel<<<(unsigned)((m + 255) / 256), 256, 0, ctx->sc>>>(m, (int)n, L, d_chain, d_pred, d_first,
-                                                                        ctx->d_st, d_st0, d_guess, d_flag);
-      if (hipGetLastError() != hipSuccess ||
-          hipMemcpyAsync(flag.data(), d_flag, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->sc) != hipSuccess ||
-          hipStreamSynchronize(ctx->sc) != hipSuccess) {
-        fail(H9G_EHIP);
-        break;
-      }
-      list.clear();
-      for (int j = 0; j < m; j++)
-        if (flag[j]) list.push_back(chain[j]);
-      if (list.empty()) break;
-      if (np > m) {                 // cannot happen (see above): a broken invariant, not a result
-        fail(H9G_ESTATE);
-        break;
-      }
-      int k = (int)list.size();
-      if (hipMemcpy(d_list, list.data(), sizeof(int) * k, hipMemcpyHostToDevice) != hipSuccess) {
-        fail(H9G_EHIP);
-        break;
-      }
-      h9g_restart_kernel<<<(unsigned)((k + 255) / 256), 256, 0, ctx->sc>>>(k, (int)n, L, d_list, d_st0, d_err0, d_guess,
-                                                                          ctx->d_st, ctx->d_err);
-      if (hipGetLastError() != hipSuccess) {
-        fail(H9G_EHIP);
-        break;
-      }
-      rerun_cells += k;
-      for (int y = 0; y < nyears && !rc && k > 0; y++) {
-        if (int r = run_year_impl(ctx, slots[y], jyear0 + y, d_list, k, d_ann_dec + (size_t)y * rows * n)) {
-          fail(r);
-          break;
-        }
-        rerun_cell_years += k;
-        rerun_launches++;
-        launch_cells.push_back(k);
-        // the cells back on their old trajectory leave the re-run
-        h9g_merge_kernel<<<(unsigned)((k + 255) / 256), 256, 0, ctx->sc>>>(
-            k, (int)n, (int)srows, d_list, ctx->d_st, ctx->d_err, ck(y), eck(y), ck(nyears - 1), eck(nyears - 1), d_flag);
-        if (hipGetLastError() != hipSuccess ||
-            hipMemcpyAsync(flag.data(), d_flag, sizeof(int) * k, hipMemcpyDeviceToHost, ctx->sc) != hipSuccess ||
-            hipStreamSynchronize(ctx->sc) != hipSuccess) {
-          fail(H9G_EHIP);
-          break;
-        }
-        int kk = 0;
-        for (int j = 0; j < k; j++)
-          if (flag[j]) list[kk++] = list[j];
-        if (kk < k && kk > 0 && hipMemcpy(d_list, list.data(), sizeof(int) * kk, hipMemcpyHostToDevice) != hipSuccess) {
-          fail(H9G_EHIP);
-          break;
-        }
-        k = kk;
-      }
-      np++;
-    }
-    if (rc) break;
-    // the last year's means stay the context's annual output; diagnostics
-    if (hipMemcpyAsync(ctx->d_ann, d_ann_dec + (size_t)(nyears - 1) * rows * n, sizeof(float) * rows * n,
-                       hipMemcpyDeviceToDevice, ctx->sc) != hipSuccess) {
-      fail(H9G_EHIP);
-      break;
-    }
-    h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)n, L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
-    if (hipGetLastError() != hipSuccess ||
-        (annual && hipMemcpyAsync(annual, d_ann_dec, sizeof(float) * (size_t)nyears * rows * n, hipMemcpyDeviceToHost,
-                                  ctx->sc) != hipSuccess))
-      fail(H9G_EHIP);
-  } while (0);
-  int src = 0;
-  if (!rc) {
-    const int had = ctx->last_err.code;
-    src = h9g_sync(ctx);   // folds the timings; the STOP of the first failing cell in context order
-    if (src > 0 && !had && ctx->last_err.cell >= 0) {
-      // its year: the first of the decade whose means it has not completed
-      std::vector<float> npp(nyears);
-      for (int y = 0; y < nyears; y++)
-        (void)hipMemcpy(&npp[y], d_ann_dec + (size_t)y * rows * n + ctx->last_err.cell, sizeof(float),
-                        hipMemcpyDeviceToHost);
-      int y = 0;
-      while (y < nyears - 1 && npp[y] == npp[y]) y++;
-      ctx->last_err.year = jyear0 + y;
+    std::vector<float> ts((size_t)L * n);
+    HIPCHK(hipMemcpy(ts.data(), ctx->d_par, sizeof(float) * ts.size(), hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < n; c++) {
+      float sum = 0.0f;
+      for (int i = 0; i < L; i++) sum = sum + ts[(size_t)i * n + c];
+      land[c] = sum > 1.0E-8f;
     }
   }
-  (void)hipStreamSynchronize(ctx->sc);
-  (void)hipFree(d_st0);
-  (void)hipFree(d_guess);
-  (void)hipFree(d_ann_dec);
-  (void)hipFree(d_err0);
-  (void)hipFree(d_chain);
-  (void)hipFree(d_pred);
-  (void)hipFree(d_first);
-  (void)hipFree(d_list);
-  (void)hipFree(d_flag);
-  (void)hipFree(d_ck);
-  (void)hipFree(d_eck);
-  ctx->dec_stats[0] = np;
-  ctx->dec_stats[1] = rerun_cells;
-  ctx->dec_stats[2] = rerun_cell_years;
-  ctx->dec_stats[3] = rerun_launches;
-  ctx->dec_launches = launch_cells;
-  if (passes) *passes = np;
-  return rc ? rc : src;
+  OrdStats S;
+  int stop_seen = 0;
+  OrdDec *P = nullptr;                     // the decade whose re-runs are still going
+  int k0 = 0;
+  for (size_t i = 0; i < decs.size(); i++) {
+    OrdDec &D = o->d[i & 1];
+    D.y0 = decs[i].first;
+    D.ny = decs[i].second;
+    D.k0 = k0;
+    k0 += D.ny;
+    D.phase = OrdDec::PASS0;
+    D.np = 0;
+    D.next_y = 0;
+    D.list.clear();
+    // the decade starts from the context's state as known now
+    HIPCHK(hipMemcpyAsync(D.st0, ctx->d_st, sizeof(float) * srows * n, hipMemcpyDeviceToDevice, ctx->sc));
+    HIPCHK(hipMemcpyAsync(D.err0, ctx->d_err, sizeof(int) * 4 * n, hipMemcpyDeviceToDevice, ctx->sc));
+    HIPCHK(hipMemcpyAsync(D.guess, ctx->d_st + (size_t)2 * L * n, sizeof(float) * (size_t)L * n,
+                          hipMemcpyDeviceToDevice, ctx->sc));
+    HIPCHK(hipMemsetAsync(D.dirty, 0, sizeof(int) * n, ctx->sc));
+    // pass 0: every cell, each year one launch, P's re-runs riding along
+    for (int y = 0; y < D.ny; y++) {
+      YearSpec ys;
+      ys.slot = slots[D.k0 + y];
+      ys.jyear = D.y0 + y;
+      const bool ride = P && P->phase == OrdDec::RERUN && g2_fits(ctx, P->list.size()) && !getenv("H9G_NO_RIDE");
+      if (ride) {
+        ys.h2 = P->list.data();
+        ys.k2 = (int)P->list.size();
+        ys.slot2 = slots[P->k0 + P->next_y];
+        ys.jyear2 = P->y0 + P->next_y;
+        ys.st2 = o->st2;
+        ys.err2 = o->err2;
+        ys.ann2 = ord_ann(ctx, *P, P->next_y);
+      }
+      if (int r = run_year_impl(ctx, ys)) return r;
+      S.ticks++;
+      HIPCHK(hipMemcpyAsync(ord_ann(ctx, D, y), ctx->d_ann, sizeof(float) * rows * n, hipMemcpyDeviceToDevice, ctx->sc));
+      HIPCHK(hipMemcpyAsync(ord_ck(ctx, D, y), ctx->d_st, sizeof(float) * srows * n, hipMemcpyDeviceToDevice, ctx->sc));
+      HIPCHK(hipMemcpyAsync(ord_eck(ctx, D, y), ctx->d_err, sizeof(int) * 4 * n, hipMemcpyDeviceToDevice, ctx->sc));
+      if (ride) {
+        S.ride_steps++;
+        S.ride_cell_years += ys.k2;
+        if (int r = ord_after_run(ctx, *P, S)) return r;
+      }
+      if (P && P->phase == OrdDec::CHECK)    // P's next pass starts in time for the next launch
+        if (int r = ord_check(ctx, *P, false, S)) return r;
+    }
+    D.np = 1;
+    if (P) {                                 // P's remaining re-runs, then its end into D's start
+      if (int r = ord_settle(ctx, *P, slots, S)) return r;
+      if (int r = ord_finish(ctx, *P, &D, annual, stop_seen)) return r;
+      S.dec_passes.push_back(P->np);
+      S.passes += P->np;
+    }
+    // D's first check (its cells whose start changed flagged too) and the
+    // year-1 re-run of every cell whose input changed
+    if (int r = ord_chain(ctx, D, land)) return r;
+    if (int r = ord_check(ctx, D, true, S)) return r;
+    if (D.phase == OrdDec::RERUN)
+      if (int r = ord_run_alone(ctx, D, slots, S)) return r;
+    if (D.phase == OrdDec::CHECK)
+      if (int r = ord_check(ctx, D, false, S)) return r;
+    P = &D;
+  }
+  if (int r = ord_settle(ctx, *P, slots, S)) return r;
+  if (int r = ord_finish(ctx, *P, nullptr, annual, stop_seen)) return r;
+  S.dec_passes.push_back(P->np);
+  S.passes += P->np;
+  // the last decade's end: the context's state, STOP records and last-year means
+  HIPCHK(hipMemcpyAsync(ctx->d_st, ord_ck(ctx, *P, P->ny - 1), sizeof(float) * srows * n, hipMemcpyDeviceToDevice,
+                        ctx->sc));
+  HIPCHK(hipMemcpyAsync(ctx->d_err, ord_eck(ctx, *P, P->ny - 1), sizeof(int) * 4 * n, hipMemcpyDeviceToDevice, ctx->sc));
+  HIPCHK(hipMemcpyAsync(ctx->d_ann, ord_ann(ctx, *P, P->ny - 1), sizeof(float) * rows * n, hipMemcpyDeviceToDevice,
+                        ctx->sc));
+  h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)n, L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
+  HIPCHK(hipGetLastError());
+  ctx->last_year = P->y0 + P->ny - 1;
+  if (passes)
+    for (size_t i = 0; i < S.dec_passes.size(); i++) passes[i] = (int32_t)S.dec_passes[i];
+  ctx->dec_stats[0] = S.passes;
+  ctx->dec_stats[1] = S.rerun_cells;
+  ctx->dec_stats[2] = S.rerun_cell_years;
+  ctx->dec_stats[3] = S.rerun_launches;
+  ctx->dec_launches = S.launch_cells;
+  const int64_t os[6] = {(int64_t)decs.size(), S.ticks, S.ride_steps, S.ride_cell_years, S.alone_steps,
+                         S.alone_cell_years};
+  std::copy(os, os + 6, ctx->ord_stats);
+  ctx->ord_passes = S.dec_passes;
+  // the first STOP of the call (h9g_last_error) or one from before it
+  return h9g_sync(ctx);
+}
+
+// The reference's decades (HYBRID9.f90:93-113: 1901-1910, 1911-1920, ...)
+// cut to [jyear0, jyear0 + nyears).
+static std::vector<std::pair<int, int>> ref_decades(int jyear0, int nyears) {
+  std::vector<std::pair<int, int>> out;
+  for (int y = jyear0, end = jyear0 + nyears; y < end;) {
+    const int d = y - 1901, start = 1901 + 10 * (d >= 0 ? d / 10 : -((9 - d) / 10));
+    const int e = std::min(start + 10, end);
+    out.push_back({y, e - y});
+    y = e;
+  }
+  return out;
+}
+
+int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int nyears, float *annual, int32_t *passes) {
+  if (nyears < 1) return H9G_EINVAL;
+  return run_ordered_impl(ctx, slots, jyear0, {{jyear0, nyears}}, annual, passes);
+}
+
+int h9g_run_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int nyears, float *annual, int32_t *passes) {
+  if (nyears < 1 || jyear0 < 1861) return H9G_EINVAL;
+  return run_ordered_impl(ctx, slots, jyear0, ref_decades(jyear0, nyears), annual, passes);
 }
 
 int h9g_set_chains(h9g_ctx *ctx, const int32_t *chain) {
@@ -1984,7 +2359,12 @@ int h9g_set_chains(h9g_ctx *ctx, const int32_t *chain) {
     return 0;
   }
   for (size_t c = 0; c < ctx->n; c++)
-    if (chain[c] < 0 || chain[c] >= (int32_t)ctx->n) return H9G_EINVAL;
+    if (chain[c] < 0 || chain[c] >= (int32_t)ctx->n) {
+      fprintf(stderr, "h9g_set_chains: cell %zu has chain id %d, not in [0, ncell): cells outside every reference "
+                      "block (shard.reference_blocks gives -1) belong to no rank's run and must be left out of the "
+                      "context\n", c, (int)chain[c]);
+      return H9G_EINVAL;
+    }
   ctx->chain_id.assign(chain, chain + ctx->n);
   return 0;
 }
@@ -1997,18 +2377,30 @@ int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n) {
   return m;
 }
 
+int h9g_ordered_stats(h9g_ctx *ctx, int64_t *out, int n) {
+  if (!ctx || !out || n < 1) return H9G_EINVAL;
+  int m = 0;
+  for (; m < n && m < 6; m++) out[m] = ctx->ord_stats[m];
+  for (size_t i = 0; m < n && i < ctx->ord_passes.size(); i++) out[m++] = ctx->ord_passes[i];
+  return m;
+}
+
+int h9g_launch_stats(h9g_ctx *ctx, double *out, int n, int reset) {
+  if (!ctx || !out || n < 1) return H9G_EINVAL;
+  if (int r = fold_events(ctx)) return r;
+  int m = 0;
+  for (int k = 1; k <= 6; k++)
+    for (int j = 0; j < 3 && m < n; j++) out[m++] = ctx->kstat[k][j];
+  if (reset)
+    for (auto &row : ctx->kstat) row[0] = row[1] = row[2] = 0.0;
+  return m;
+}
+
 int h9g_sync(h9g_ctx *ctx) {
   if (!ctx) return H9G_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamSynchronize(ctx->sx));
-  HIPCHK(hipStreamSynchronize(ctx->sc));
-  for (int i = 0; i < ctx->nev; i++) {
-    float ms = 0.0f;
-    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0[i], ctx->ev1[i]));
-    ctx->total_ms += ms;
-    ctx->last_ms = ms;
-  }
-  ctx->nev = 0;
+  if (int r = fold_events(ctx)) return r;
 #if defined(H9G_STAMPS)
   if (ctx->d_stamps && ctx->kind == 1) {   // mean shader cycles per wave and substep, by phase
     const size_t nw = (ctx->n + H9G_PCPW - 1) / H9G_PCPW;

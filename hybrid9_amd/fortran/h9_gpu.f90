@@ -175,6 +175,25 @@ INTERFACE
     INTEGER(C_INT32_T), INTENT(OUT) :: passes
     INTEGER(C_INT) :: h9g_run_decade_ordered
   END FUNCTION
+  ! The same over several decades at once (every year's forcing resident),
+  ! the decades overlapping on the device; passes: one per decade.
+  FUNCTION h9g_run_ordered (ctx, slots, jyear0, nyears, annual, passes) &
+           BIND(C, NAME='h9g_run_ordered')
+    IMPORT :: C_PTR, C_INT, C_INT32_T, C_FLOAT
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT32_T), INTENT(IN) :: slots (*)
+    INTEGER(C_INT), VALUE :: jyear0, nyears
+    REAL(C_FLOAT), INTENT(OUT) :: annual (*)
+    INTEGER(C_INT32_T), INTENT(OUT) :: passes (*)
+    INTEGER(C_INT) :: h9g_run_ordered
+  END FUNCTION
+  FUNCTION h9g_ordered_stats (ctx, out, n) BIND(C, NAME='h9g_ordered_stats')
+    IMPORT :: C_PTR, C_INT, C_INT64_T
+    TYPE(C_PTR), VALUE :: ctx
+    INTEGER(C_INT64_T), INTENT(OUT) :: out (*)
+    INTEGER(C_INT), VALUE :: n
+    INTEGER(C_INT) :: h9g_ordered_stats
+  END FUNCTION
   FUNCTION h9g_set_chains (ctx, chain) BIND(C, NAME='h9g_set_chains')
     IMPORT :: C_PTR, C_INT, C_INT32_T
     TYPE(C_PTR), VALUE :: ctx
@@ -313,6 +332,13 @@ INTERFACE
     TYPE(C_PTR), VALUE :: ctx
     INTEGER(C_INT), VALUE :: reset
     REAL(C_DOUBLE) :: h9g_total_kernel_ms
+  END FUNCTION
+  FUNCTION h9g_launch_stats (ctx, out, n, reset) BIND(C, NAME='h9g_launch_stats')
+    IMPORT :: C_PTR, C_INT, C_DOUBLE
+    TYPE(C_PTR), VALUE :: ctx
+    REAL(C_DOUBLE), INTENT(OUT) :: out (*)
+    INTEGER(C_INT), VALUE :: n, reset
+    INTEGER(C_INT) :: h9g_launch_stats
   END FUNCTION
 END INTERFACE
 

@@ -233,7 +233,9 @@ IF (cell_order /= 0) THEN
   ALLOCATE (annual_dec (ncell, 12 + L, 10))
   dsyr = year0
   DO WHILE (dsyr < year0 + nyears)
-    deyr = MIN (1901 + 10 * ((dsyr - 1901) / 10) + 9, year0 + nyears - 1)
+    ! (FLOOR, not integer division, which truncates toward zero: before 1901
+    ! the decades are 1891-1900, 1881-1890, ...)
+    deyr = MIN (1901 + 10 * FLOOR (REAL (dsyr - 1901) / 10.0) + 9, year0 + nyears - 1)
     ndec = deyr - dsyr + 1
     DO k = 1, ndec
       slots (k) = k - 1

@@ -166,6 +166,20 @@ int h9g_get_errors(h9g_ctx *ctx, int32_t *rec);
  * context order (h9g_last_error, with its year). */
 int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0,
                            int nyears, float *annual, int32_t *passes);
+/* The reference's decade loop over several decades: years jyear0 ..
+ * jyear0+nyears-1 (the forcing of year jyear0+k in slots[k], every year's
+ * slot resident for the whole call) cut into the reference's decades
+ * (1901-1910, 1911-1920, ...), each run as h9g_run_decade_ordered runs
+ * one, with the same results bit for bit.  The decades overlap on the
+ * device: a decade's first pass starts as soon as the previous decade's
+ * first pass and year-1 re-run are done, and that decade's remaining
+ * re-runs ride in its year launches.  annual: (nyears,
+ * 12+L, ncell) host (may be NULL); passes (may be NULL): one int32 per
+ * decade.  A cell that STOPs leaves the later decades' chains (the
+ * reference would end the program there; h9g_last_error reports the first
+ * STOP in decade then context order).  Synchronous. */
+int h9g_run_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0, int nyears,
+                    float *annual, int32_t *passes);
 /* Splits the context's cells into independent chains for
  * h9g_run_decade_ordered, one per reference MPI rank: chain[c] (ncell
  * int32, 0 <= id < ncell) is the rank whose block holds cell c (INIT.f90:
@@ -180,6 +194,11 @@ int h9g_set_chains(h9g_ctx *ctx, const int32_t *chain);
  * is its previous run's again), then the cells of each re-run launch in
  * order.  Returns the count written (<= 4 + launches). */
 int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n);
+/* How the last ordered call overlapped its decades: out[0..n) of decades,
+ * year launches of the first passes, re-run years that rode in them and
+ * their cell-years, re-run years launched alone and their cell-years, then
+ * each decade's passes.  Returns the count written. */
+int h9g_ordered_stats(h9g_ctx *ctx, int64_t *out, int n);
 
 /* --- LCLIM single-site path (HYBRID9.f90:339-480) ---------------------- */
 /* Runs nday days of the site path for every cell of the context: per
@@ -286,6 +305,11 @@ int h9g_get_params(h9g_ctx *ctx, float *theta_s, float *hksat, float *bsw,
 float h9g_last_kernel_ms(h9g_ctx *ctx);
 double h9g_total_kernel_ms(h9g_ctx *ctx, int reset);
 const char *h9g_kernel_name(h9g_ctx *ctx);
+/* Per kernel kind 1..6 (pair, solo, solo+pair, pair2, pair11, pair1 -- the
+ * one-column kernel of short re-run lists), 3 doubles each: year launches,
+ * cell-years and device ms since the last reset (synchronises).  Returns the
+ * count written (<= 18). */
+int h9g_launch_stats(h9g_ctx *ctx, double *out, int n, int reset);
 /* Digest of the sources and compile flags of this library (16 hex digits;
  * hybrid9_amd/build.py build_id).  Profiles record it, and the bench
  * attaches counters only to the build they were measured on.  No GPU. */

@@ -128,29 +128,36 @@ def test_oracle_cell_order_matches_reference_golden():
 # GPU: the product in the reference's order (h9g_run_decade_ordered)
 # --------------------------------------------------------------------------
 @pytest.mark.gpu
+@pytest.mark.parametrize("pipelined", [True, False], ids=["run_ordered", "per_decade"])
 @pytest.mark.parametrize("name", ["co_c1_30yr", "co_band"])
-def test_gpu_cell_order_matches_reference(name):
+def test_gpu_cell_order_matches_reference(name, pipelined):
+    """h9g_run_ordered (the decades overlapping: a decade's re-runs ride in
+    the next decade's year launches) and h9g_run_decade_ordered (one call
+    per decade) both reproduce the reference's own order bit for bit."""
     import hybrid9_amd as h
     meta, inp, exp = load_golden(name)
-    out = h.run_cell_order(**inp)
+    out = h.run_cell_order(pipelined=pipelined, **inp)
     assert out["rc"] == 0, out["err"]
     assert same_bits(out["annual"], exp["annual"])
     assert same_bits(out["state"], exp["state"])
     yrs = [w["rerun_cell_years"] for w in out["work"]]
     print(f"{name}: {meta['ncell']} cells x {meta['nyears']} years bit-identical to the reference's cell order; "
           f"decade passes {out['passes']}, cell-years re-run {yrs}, re-run launches "
-          f"{[w['rerun_launches'] for w in out['work']]}")
+          f"{[w['rerun_launches'] for w in out['work']]}" + (f", overlap {out['overlap']}" if pipelined else ""))
+    if pipelined and meta["nyears"] > 10:
+        assert out["overlap"]["rerun_years_riding"] > 0     # the overlap path ran
 
 
 @pytest.mark.gpu
-def test_gpu_cell_order_blocks_match_reference():
+@pytest.mark.parametrize("pipelined", [True, False], ids=["run_ordered", "per_decade"])
+def test_gpu_cell_order_blocks_match_reference(pipelined):
     """One context holding the 4 reference ranks' blocks as 4 chains
     (h9g_set_chains) reproduces the reference's 4-process run bit for bit;
     so does each rank's block run alone (one GPU per rank)."""
     import hybrid9_amd as h
     meta, inp, exp = load_golden("co_c1_blocks4")
     rank = np.asarray(meta["rank"])
-    out = h.run_cell_order(chains=rank, **inp)
+    out = h.run_cell_order(chains=rank, pipelined=pipelined, **inp)
     assert out["rc"] == 0, out["err"]
     assert same_bits(out["annual"], exp["annual"])
     assert same_bits(out["state"], exp["state"])
@@ -161,7 +168,7 @@ def test_gpu_cell_order_blocks_match_reference():
         sel = np.where(rank == r)[0]
         sub = dict(inp, params={k: v[sel] for k, v in inp["params"].items()},
                    forcing=np.ascontiguousarray(inp["forcing"][:, :, sel]))
-        o = h.run_cell_order(**sub)
+        o = h.run_cell_order(pipelined=pipelined, **sub)
         assert o["rc"] == 0
         assert same_bits(o["annual"], exp["annual"][:, :, sel])
         got = refcase.unpack_state(o["state"], sel.size, L)
