@@ -351,7 +351,7 @@ class NcFed:
         return {"source": "synthetic PGF v2.1 netCDF-4 files (one chunk per day, shuffle + deflate 4)",
                 "file_bytes_per_year": int(self.bytes), "write_s": self.write_s,
                 "read_s_per_year_sync": self.read_s, "read_stages": self.read_stages,
-                "io_threads": int(os.environ.get("H9G_IO_THREADS", "0")) or min(16, os.cpu_count() or 1),
+                "io_threads": self.read_stages.get("threads"), "host": host_cpu(),
                 "slots": 2, "reader": "h9g_nc_forcing_prefetch (direct chunk reads, libdeflate, host pool)"}
 
 
@@ -628,7 +628,7 @@ def main():
     # and the year-1 re-runs); the one-column kernel of short re-run lists
     # is reported beside it
     kname = ctx.kernel_name()
-    main_kind = {1: "pair", 2: "solo", 3: "mixed", 4: "pair2", 5: "pair11"}[ctx.kind_id()]
+    main_kind = {1: "pair", 2: "solo", 3: "mixed", 4: "pair2", 5: "pair11", 6: "pair1"}[ctx.kind_id()]
     if args.order == "cell" and main_kind in launches:
         ml = launches[main_kind]
         n_launch, launch_ms, cy_launch = ml["launches"], ml["ms"], ml["cell_years"] / max(1, ml["launches"])

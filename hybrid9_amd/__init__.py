@@ -490,11 +490,11 @@ class Context:
 
     def kind_id(self) -> int:
         """The context's year kernel as h9g_launch_stats numbers it: 1 pair,
-        2 solo, 3 solo rounds + pair, 4 pair2, 5 pair11."""
+        2 solo, 3 solo rounds + pair, 4 pair2, 5 pair11, 6 pair1."""
         name = self.kernel_name()
         if "+" in name:
             return 3
-        for prefix, k in (("h9g_solo_", 2), ("h9g_pair2_", 4), ("h9g_pair11_", 5)):
+        for prefix, k in (("h9g_solo_", 2), ("h9g_pair2_", 4), ("h9g_pair11_", 5), ("h9g_pair1_", 6)):
             if name.startswith(prefix):
                 return k
         return 1

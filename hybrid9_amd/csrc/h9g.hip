@@ -297,9 +297,10 @@ h9g_pair2_kernel(const KArgs a, const G g) {
 // lanes past the pairs help in the per-layer phases, which then take 2
 // rounds instead of 5 at L = 10 (hydrology_pair helpers), and the wave's LDS
 // block halves, so every reciprocal field fits at 3 waves per SIMD.  Twice
-// the waves of 22-column ones for the same cells: l10_kind takes it for
-// shards whose 11-column waves still fit one round of 3 per SIMD (the
-// 8-GPU config-5 shard, 33,750 cells: 3,069 waves for 3,072 slots).
+// the waves of 22-column ones for the same cells.  Measured on the 8-GPU
+// config-5 shard (33,750 cells: 3,069 waves for 3,072 slots) it lost to
+// pair2, so l10_kind never picks it; H9G_KERNEL=pair11
+// selects it, and the GPU tests run it.
 #define H9G_PCPW11 11
 template <int L, class G>
 __global__ void __launch_bounds__(64 * H9G_PWAVES) __attribute__((amdgpu_waves_per_eu(3, 3)))
@@ -1076,8 +1077,9 @@ struct h9g_ctx {
   int ncu = 256;
   int sort = 1;                   // H9G_SORT=0: identity order
   size_t sv_bytes = 0;
-  int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel, 3: both, 4: h9g_pair2_kernel (L = 10)
-                       // (H9G_KERNEL=pair|solo|mixed|pair2; default by L and the shard size, l10_kind)
+  int kind = 1;        // 1: h9g_pair_kernel, 2: h9g_solo_kernel, 3: both, 4: h9g_pair2_kernel (L = 10),
+                       // 5: h9g_pair11_kernel, 6: h9g_pair1_kernel (H9G_KERNEL=pair|solo|mixed|pair2|pair11|
+                       // pair1; default by L and the shard size, l10_kind)
   size_t n_solo = 0;   // kind 3: cells [0, n_solo) run on the solo kernel, the rest on the pair kernel
   size_t ios = 0;      // slots of the slot-ordered buffers (d_perm, d_forc_s, d_ann_s): the cells + H9G_G2_MAX
   size_t stamp_words = 0;
@@ -1400,7 +1402,7 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     h9g_destroy(ctx);
     return nullptr;
   }
-  static const char *names[6][2][3] = {
+  static const char *names[7][2][3] = {
       {{"", "", ""}, {"", "", ""}},
       {{"h9g_pair_kernel<8,GeoR>", "h9g_pair_kernel<8,GeoC<8,24>>", "h9g_pair_kernel<8,GeoC<8,48>>"},
        {"h9g_pair_kernel<10,GeoR>", "h9g_pair_kernel<10,GeoC<10,24>>", "h9g_pair_kernel<10,GeoC<10,48>>"}},
@@ -1414,7 +1416,9 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
       {{"", "", ""},
        {"h9g_pair2_kernel<10,GeoR>", "h9g_pair2_kernel<10,GeoC<10,24>>", "h9g_pair2_kernel<10,GeoC<10,48>>"}},
       {{"h9g_pair11_kernel<8,GeoR>", "h9g_pair11_kernel<8,GeoC<8,24>>", "h9g_pair11_kernel<8,GeoC<8,48>>"},
-       {"h9g_pair11_kernel<10,GeoR>", "h9g_pair11_kernel<10,GeoC<10,24>>", "h9g_pair11_kernel<10,GeoC<10,48>>"}}};
+       {"h9g_pair11_kernel<10,GeoR>", "h9g_pair11_kernel<10,GeoC<10,24>>", "h9g_pair11_kernel<10,GeoC<10,48>>"}},
+      {{"h9g_pair1_kernel<8,GeoR>", "h9g_pair1_kernel<8,GeoC<8,24>>", "h9g_pair1_kernel<8,GeoC<8,48>>"},
+       {"h9g_pair1_kernel<10,GeoR>", "h9g_pair1_kernel<10,GeoC<10,24>>", "h9g_pair1_kernel<10,GeoC<10,48>>"}}};
   // default: the pair kernel at L = 8; at L = 10 the kernel that needs less
   // time for this many columns (l10_kind)
   if (const char *se = getenv("H9G_SORT")) ctx->sort = atoi(se) != 0;
@@ -1445,6 +1449,8 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
     ctx->kind = 4;
   else if (kenv && strcmp(kenv, "pair11") == 0)
     ctx->kind = 5;
+  else if (kenv && strcmp(kenv, "pair1") == 0)   // the one-column kernel for every launch (tests, probes)
+    ctx->kind = 6;
   else if (kenv && strcmp(kenv, "mixed") == 0) {
     // forced split (tests): H9G_SPLIT cells on the solo kernel, else the model's
     ctx->kind = 3;
@@ -2402,8 +2408,8 @@ int h9g_sync(h9g_ctx *ctx) {
   HIPCHK(hipStreamSynchronize(ctx->sx));
   if (int r = fold_events(ctx)) return r;
 #if defined(H9G_STAMPS)
-  if (ctx->d_stamps && ctx->kind == 1) {   // mean shader cycles per wave and substep, by phase
-    const size_t nw = (ctx->n + H9G_PCPW - 1) / H9G_PCPW;
+  if (ctx->d_stamps && (ctx->kind == 1 || ctx->kind == 5 || ctx->kind == 6)) {   // mean shader cycles per wave and substep, by phase
+    const size_t cw = (size_t)pair_wave_cols(ctx->kind), nw = (ctx->n + cw - 1) / cw;
     std::vector<unsigned> st(8 * nw);
     HIPCHK(hipMemcpy(st.data(), ctx->d_stamps, sizeof(unsigned) * 8 * nw, hipMemcpyDeviceToHost));
     double sum[8] = {0}, tot = 0;

@@ -37,6 +37,7 @@
 #include <mutex>
 #include <type_traits>
 #include <string>
+#include <sched.h>
 #include <thread>
 #include <vector>
 
@@ -571,15 +572,22 @@ struct Chunked {               // a (time, lat, lon) field stored as filtered ch
   }
 };
 
-// Host threads of the ingest pool: $H9G_IO_THREADS, else the hardware's,
-// at most 16 (a GPU's share of the host on the MI355X boxes).
+// Host threads of the ingest pool: $H9G_IO_THREADS, else the CPUs this
+// process may run on (its affinity mask: the lease), at most
+// $OMP_NUM_THREADS when that is set (the MI355X boxes set it to a GPU's
+// share, 16), else at most 16.
 int io_threads() {
   if (const char *e = getenv("H9G_IO_THREADS")) {
     const int v = atoi(e);
     if (v > 0) return v;
   }
-  const unsigned hc = std::thread::hardware_concurrency();
-  return (int)std::max(1u, std::min(16u, hc ? hc : 1u));
+  unsigned hc = std::thread::hardware_concurrency();
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof set, &set) == 0) hc = (unsigned)CPU_COUNT(&set);
+  unsigned cap = 16;
+  if (const char *e = getenv("OMP_NUM_THREADS"))
+    if (atoi(e) > 0) cap = (unsigned)atoi(e);
+  return (int)std::max(1u, std::min(cap, hc ? hc : 1u));
 }
 
 // Runs job(i, worker) for i in [0, n) on the pool; false if any job failed.

@@ -3,10 +3,12 @@
 The reference decomposes the globe into sqrt(P) x sqrt(P) equal blocks, one
 per MPI rank, and the ranks never communicate during compute
 (``INIT.f90:271-274,427-456``; ``HYBRID9.f90:120-295``).  Cells are
-independent under isolated-cell semantics, so here a shard is a contiguous
+independent under isolated-cell semantics, so there a shard is a contiguous
 range of the compacted land-cell list -- balanced, unlike square blocks that
-leave ocean-only ranks idle.  The only cross-GPU traffic is the all-reduce of
-the FP64 global diagnostics (``h9g_get_diagnostics``) once per year.
+leave ocean-only ranks idle.  In the reference's own cell order a block is
+one chain, so a rank takes whole blocks (``blocks_of_rank``).  The only
+cross-GPU traffic is the all-reduce of the FP64 global diagnostics
+(``h9g_get_diagnostics``) once per year or per ordered call.
 """
 from __future__ import annotations
 
@@ -43,6 +45,20 @@ def reference_blocks(gid, nx: int, ny: int, num_procs: int) -> np.ndarray:
     bx, by = ix // lon_c, iy // lat_c
     r = by * nb + bx
     return np.where((bx < nb) & (by < nb), r, -1).astype(np.int32)
+
+
+def blocks_of_rank(blocks, rank: int, world: int) -> np.ndarray:
+    """The cells (indices into ``blocks``, ascending) a GPU rank takes in the
+    reference's cell order: whole reference blocks (``reference_blocks``),
+    block b to rank b mod world.  A block is one chain of the reference's
+    order (one MPI rank's cell loop, HYBRID9.f90:120-295), so the ranks'
+    chains are independent and no collective joins them; cells outside
+    every block (-1) belong to no rank.  Give the rank's context
+    ``h9g_set_chains`` with the blocks' ids."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    b = np.asarray(blocks)
+    return np.where((b >= 0) & (b % world == rank))[0]
 
 
 def weak_seed(base_seed: int, rank: int) -> int:

@@ -63,7 +63,11 @@ def load_golden(name):
     n = meta["ncell"]
     if meta["kind"] in ("synth", "bench_stop", "cell_order"):
         gid = np.asarray(meta["gid"], dtype=np.int64)
-        p, f = synth_inputs(gid, meta["year0"], meta["nyears"], L, meta["seed"])
+        if meta.get("grid") == "025":           # 0.25 deg cells (config 5)
+            from tests.golden.make_golden import l10_inputs
+            p, f = l10_inputs(gid, meta["year0"], meta["nyears"], meta["seed"])
+        else:
+            p, f = synth_inputs(gid, meta["year0"], meta["nyears"], L, meta["seed"])
         assert digest(packed_params(p), f) == meta["input_sha256"], "synthetic inputs drifted"
         state0 = None
     elif meta["kind"] == "spinup":

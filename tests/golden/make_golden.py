@@ -343,7 +343,7 @@ def rel_bound(a, b):
     return float(r.max()) if r.size else 0.0
 
 
-def cell_order_case(name, gid, *, year0=1901, nyears=30, nisurf=48, grow_on=1, split=None):
+def cell_order_case(name, gid, *, year0=1901, nyears=30, nisurf=48, grow_on=1, split=None, L=8):
     """The reference as it really runs: h9ref's cell_order
     mode, decade -> cell -> year with smp carried from cell to cell
     (HYBRID9.f90:93-130, HYDROLOGY.f90:270-275, SHARED.f90:198), cells in
@@ -352,13 +352,13 @@ def cell_order_case(name, gid, *, year0=1901, nyears=30, nisurf=48, grow_on=1, s
     (split) how far the reference itself moves when its cells are cut into
     two ranks (two chains, INIT.f90:271-274)."""
     gid = np.asarray(gid, dtype=np.int64)
-    p, f = synth_inputs(gid, year0, nyears)
-    kw = dict(zi=synth.ZI_L8, params=p, forcing=f, nisurf=nisurf, year0=year0, nyears=nyears,
+    p, f = synth_inputs(gid, year0, nyears) if L == 8 else l10_inputs(gid, year0, nyears)
+    zi = synth.ZI_L8 if L == 8 else synth.ZI_L10
+    kw = dict(zi=zi, params=p, forcing=f, nisurf=nisurf, year0=year0, nyears=nyears,
               grow_on=grow_on)
     co = refcase.run_case(cell_order=True, **kw)
     iso = refcase.run_case(**kw)
     ai, ac = iso["annual"], co["annual"]
-    L = 8
     fields = refcase.annual_fields(L)
     pick = [fields.index(k) for k in ["rnf", "theta_total"] + [f"theta{i + 1}" for i in range(L)]]
     diff_cells = np.any(np.any(ai.view(np.uint32) != ac.view(np.uint32), axis=0), axis=0)
@@ -376,7 +376,7 @@ def cell_order_case(name, gid, *, year0=1901, nyears=30, nisurf=48, grow_on=1, s
         half = gid.size // 2
         parts = []
         for sl in (slice(0, half), slice(half, gid.size)):
-            parts.append(refcase.run_case(cell_order=True, zi=synth.ZI_L8,
+            parts.append(refcase.run_case(cell_order=True, zi=zi,
                                           params={k: v[sl] for k, v in p.items()},
                                           forcing=np.ascontiguousarray(f[:, :, sl]), nisurf=nisurf, year0=year0,
                                           nyears=nyears, grow_on=grow_on)["annual"])
@@ -385,10 +385,12 @@ def cell_order_case(name, gid, *, year0=1901, nyears=30, nisurf=48, grow_on=1, s
                            cells_differing=int(np.any(np.any(a2.view(np.uint32) != ac.view(np.uint32), axis=0),
                                                       axis=0).sum()))
     meta = dict(name=name, kind="cell_order", seed=synth.SEED, gid=gid.tolist(), L=L, ncell=int(gid.size),
-                year0=year0, nyears=nyears, nisurf=nisurf, grow_on=grow_on, zi=synth.ZI_L8.tolist(),
+                year0=year0, nyears=nyears, nisurf=nisurf, grow_on=grow_on, zi=zi.tolist(),
+                grid="05" if L == 8 else "025",
                 input_sha256=digest(packed_params(p), f), isolated_vs_cell_order=iso_bound,
                 two_ranks_vs_one=split_bound,
-                generator="oracle/_ref/h9ref cell_order=1 (reference HYDROLOGY.f90/GROW.f90, amdflang -O2; "
+                generator=f"oracle/_ref/{refcase.ref_bin(L).name} cell_order=1 (reference HYDROLOGY.f90/GROW.f90"
+                          f"{'' if L == 8 else ' with nsoil_layers_max=10, Nlevgrnd=11'}, amdflang -O2; "
                           "decade -> cell -> year, smp carried between cells)")
     np.savez_compressed(OUT / f"{name}.npz", meta=np.array(json.dumps(meta)), annual=ac,
                         state=refcase.pack_state(co["state"], L))
@@ -462,6 +464,19 @@ def cell_order_stop_case(name="co_stop", year0=1901, nisurf=24, grow_on=1):
     print(f"{name}: reference STOP in cell order {info}")
 
 
+def main_cell_order_configs():
+    """The ordered mode on the configurations the bench quotes it on
+    (VERDICT r05 #2): config 2 (0.5 deg, GROW off, NS=48) on a row band over
+    1901-1930, so the bench's timed decades are covered, and config 5
+    (0.25 deg, L = 10, NS = 24, GROW on) on a row band over 1901-1920."""
+    land = synth.land_cells()
+    rows = land // synth.NX05
+    cell_order_case("co_c2_band", land[(rows >= 130) & (rows < 138)], nyears=30, grow_on=0)
+    l4 = synth.land_cells(synth.NX025, synth.NY025, synth.NLAND025)
+    r4 = l4 // synth.NX025
+    cell_order_case("co_c5_band", l4[(r4 >= 300) & (r4 < 304)], nyears=20, nisurf=24, grow_on=1, L=10)
+
+
 def main_cell_order():
     g10 = np.array([(80 + j) * synth.NX05 + 400 + i for j in range(10) for i in range(10)])
     # config 1's grid over three decades (1901-1930)
@@ -473,6 +488,7 @@ def main_cell_order():
     # config 1's grid as the reference runs it on 4 MPI ranks (2 x 2 blocks of 5 x 5)
     cell_order_blocks_case("co_c1_blocks4", g10, 10, 10, 4)
     cell_order_stop_case()
+    main_cell_order_configs()
 
 
 def site_inputs(gid, L, nisurf, years, events, seed=synth.SEED, soils="synth", ppt_scale=1.0):

@@ -23,12 +23,13 @@ def _gpu_run(inp, L):
                  grow_on=bool(inp["grow_on"]), state0=inp["state0"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "pair11", "solo", "mixed"])
+@pytest.mark.parametrize("kernel", ["pair", "pair11", "pair1", "solo", "mixed"])
 @pytest.mark.parametrize("name", golden_names(kind=("synth", "explicit", "spinup")))
 def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
-    """The year kernels (two lanes per column = the default, with 22 or 11
-    columns per wave; one lane), and two in one run (cells [0, 37) on the
-    solo kernel, the rest on pair)."""
+    """The year kernels (two lanes per column = the default, with 22, 11 or
+    1 column per wave -- the last is the cell order's kernel for short
+    re-run lists; one lane), and two in one run (cells [0, 37) on the solo
+    kernel, the rest on pair)."""
     monkeypatch.setenv("H9G_KERNEL", kernel)
     monkeypatch.setenv("H9G_SPLIT", "37")
     meta, inp, exp = load_golden(name)
@@ -38,7 +39,7 @@ def test_gpu_matches_reference_golden(name, kernel, monkeypatch):
     assert same_bits(out["state"], exp["state"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "pair11", "solo"])
+@pytest.mark.parametrize("kernel", ["pair", "pair11", "pair1", "solo"])
 @pytest.mark.parametrize("name", golden_names(kind=("stop",)))
 def test_gpu_reproduces_reference_stop(name, kernel, monkeypatch):
     monkeypatch.setenv("H9G_KERNEL", kernel)
@@ -72,7 +73,7 @@ def test_config4_spinup_decades_carry_state():
     assert same_bits(d2["state"], exp["state"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "pair2", "pair11", "solo", "mixed"])
+@pytest.mark.parametrize("kernel", ["pair", "pair2", "pair11", "pair1", "solo", "mixed"])
 def test_config5_l10_matches_reference_golden(kernel, monkeypatch):
     """Config 5 (0.25 deg, L = 10, NS = 24, GROW) against the reference
     rebuilt with nsoil_layers_max = 10: every annual mean (NaN for the cell
@@ -120,7 +121,7 @@ def test_gpu_reproduces_bench_stop(kernel, monkeypatch):
     assert same_bits(refcase.pack_state(st, meta["L"]), exp["state_ok"])
 
 
-@pytest.mark.parametrize("kernel", ["pair", "pair11", "solo"])
+@pytest.mark.parametrize("kernel", ["pair", "pair11", "pair1", "solo"])
 def test_gpu_nan_parameter_cells_match_oracle(kernel, monkeypatch):
     """Cells with missing soil data (NaN Fmax, a NaN layer parameter) run
     the year with NaN state, so every deferred special-case check of the
