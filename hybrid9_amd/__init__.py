@@ -385,9 +385,9 @@ class Context:
         out = (C.c_int64 * 64)()
         m = _check(self._lib.h9g_ordered_stats(self._h, out, 64), "h9g_ordered_stats")
         keys = ("decades", "first_pass_launches", "rerun_years_riding", "rerun_cell_years_riding",
-                "rerun_years_alone", "rerun_cell_years_alone")
+                "rerun_years_alone", "rerun_cell_years_alone", "cells_left_out_of_first_pass")
         d = {k: int(out[i]) for i, k in enumerate(keys)}
-        d["passes"] = [int(out[i]) for i in range(6, m)]
+        d["passes"] = [int(out[i]) for i in range(len(keys), m)]
         return d
 
     def launch_stats(self, reset: bool = False) -> dict:

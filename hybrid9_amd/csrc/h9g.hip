@@ -63,9 +63,6 @@ static const double h_log2tab[32] = H9M_POWF_LOG2_TAB_INIT;
 #define H9G_PLANES (2 * H9G_PCPW)
 #define H9G_PWAVES 4
 #define NEVT 64
-// Cells a year launch carries at most in its second group (KArgs::split);
-// the slot-ordered forcing and annual buffers have that much slack.
-#define H9G_G2_MAX 1024
 static size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
 // ---------------------------------------------------------------------------
@@ -604,12 +601,15 @@ __global__ void __launch_bounds__(256) h9g_merge_kernel(int m, int n, int rows, 
 // (measured with H9G_COUNT_BRANCH at 1906-1907: 84% of the wave-substeps ran
 // the aquifer node, 81% the recharge).  Block x sorts the slots of XCD x's
 // workgroups of the year launch over [c0, cend) with cpb cells per workgroup
-// (xcd_vwg), so no cell leaves its XCD's range.
+// (xcd_vwg), so no cell leaves its XCD's range.  list (may be null): the
+// slots hold the cells list[c0 .. cend) instead of c0 .. cend (the cell
+// order's re-run lists; round 6).
 #define H9G_SORT_THREADS 512
 template <int L, class G>
 __global__ void __launch_bounds__(H9G_SORT_THREADS)
     h9g_sort_kernel(int n, int c0, int cend, int cpb, const float *__restrict__ st, const int *__restrict__ err,
-                    const int *__restrict__ hist, int nsub, int *__restrict__ perm, const G g) {
+                    const int *__restrict__ hist, int nsub, int *__restrict__ perm, const int *__restrict__ list,
+                    const G g) {
   constexpr int NK = L + 10;
   constexpr int NTH = H9G_SORT_THREADS;
   __shared__ int cnt[NK][NTH];
@@ -640,7 +640,7 @@ __global__ void __launch_bounds__(H9G_SORT_THREADS)
 #pragma unroll
   for (int k = 0; k < NK; k++) loc[k] = 0;
   for (int c = b; c < e; c++) {
-    const int k = key(c);
+    const int k = key(list ? list[c] : c);
 #pragma unroll
     for (int j = 0; j < NK; j++) loc[j] += (j == k);
   }
@@ -669,12 +669,13 @@ __global__ void __launch_bounds__(H9G_SORT_THREADS)
 #pragma unroll
   for (int k = 0; k < NK; k++) loc[k] = base[k] + cnt[k][t];
   for (int c = b; c < e; c++) {
-    const int k = key(c);
+    const int cell = list ? list[c] : c;
+    const int k = key(cell);
     int pos = 0;
 #pragma unroll
     for (int j = 0; j < NK; j++)
       if (j == k) pos = loc[j]++;
-    perm[p0 + pos] = c;
+    perm[p0 + pos] = cell;
   }
 }
 
@@ -1063,6 +1064,7 @@ struct h9g_ctx {
   int *d_slow = nullptr;
   float *d_sv = nullptr;          // pair kernel day-snapshot blocks
   int *d_perm = nullptr;          // cell order of the year kernel (h9g_sort_kernel)
+  int *d_perm2 = nullptr;         // a launch's second group as listed (sorted into d_perm)
   float *d_forc_s = nullptr;      // the year's forcing in slot order (h9g_perm_forcing_kernel)
   float *d_ann_s = nullptr;       // the year kernel's annual sums in slot order
   unsigned *d_aqbits = nullptr;   // H9G_DUMP_AQ builds: day-level water-table record of the last year
@@ -1081,13 +1083,13 @@ struct h9g_ctx {
                        // 5: h9g_pair11_kernel, 6: h9g_pair1_kernel (H9G_KERNEL=pair|solo|mixed|pair2|pair11|
                        // pair1; default by L and the shard size, l10_kind)
   size_t n_solo = 0;   // kind 3: cells [0, n_solo) run on the solo kernel, the rest on the pair kernel
-  size_t ios = 0;      // slots of the slot-ordered buffers (d_perm, d_forc_s, d_ann_s): the cells + H9G_G2_MAX
+  size_t ios = 0;      // slots of the slot-ordered buffers (d_perm, d_forc_s, d_ann_s): twice the cells
   size_t stamp_words = 0;
   int ev_kind[NEVT] = {};         // kernel kind and cell-years of each timed launch
   int64_t ev_cells[NEVT] = {};
   double kstat[8][3] = {};        // per kernel kind: launches, cell-years, ms (h9g_launch_stats)
   struct OrdBufs *ord = nullptr;  // h9g_run_ordered's decade buffers
-  int64_t ord_stats[6] = {};      // last ordered call (h9g_ordered_stats)
+  int64_t ord_stats[7] = {};      // last ordered call (h9g_ordered_stats)
   std::vector<int64_t> ord_passes;
 };
 
@@ -1226,6 +1228,7 @@ void h9g_destroy(h9g_ctx *ctx) {
   (void)hipFree(ctx->d_stamps);
   (void)hipFree(ctx->d_slow);
   (void)hipFree(ctx->d_perm);
+  (void)hipFree(ctx->d_perm2);
   (void)hipFree(ctx->d_forc_s);
   (void)hipFree(ctx->d_ann_s);
   (void)hipFree(ctx->d_hist);
@@ -1281,13 +1284,13 @@ static size_t ord_bytes(size_t n, size_t L, size_t ny) {
   const size_t srows = 4 * L + 9, rows = 12 + L;
   return 2 * (sizeof(float) * (srows + L + ny * (rows + srows)) * n + sizeof(int) * (4 + 4 * ny + 1) * n +
               sizeof(int) * 5 * (n + 1)) +
-         sizeof(float) * srows * n + sizeof(int) * 4 * n;
+         sizeof(float) * srows * n + sizeof(int) * (4 * n + n + 1);
 }
 
 size_t h9g_config_bytes(const h9g_config *cfg) {
   if (!cfg || cfg->ncell <= 0 || cfg->nlayers < 1 || cfg->max_days < 1 || cfg->nslots < 1) return 0;
   const size_t n = (size_t)cfg->ncell, L = (size_t)cfg->nlayers;
-  const size_t ios = round_up(n, H9G_PCPW) + H9G_G2_MAX;
+  const size_t ios = 2 * round_up(n, H9G_PCPW) + 64;
   // the largest launch's day-snapshot blocks: the 11-column kernel's over
   // every cell, or the one-column kernel's over H9G_PAIR1_MAX listed cells
   const size_t blocks = std::max((ios + (size_t)H9G_PCPW11 * H9G_PWAVES - 1) / ((size_t)H9G_PCPW11 * H9G_PWAVES),
@@ -1296,7 +1299,7 @@ size_t h9g_config_bytes(const h9g_config *cfg) {
   // (h9g_run_year, allocated on first use), the ordered mode's decade
   // buffers (h9g_run_ordered, decades of up to 10 years)
   return sizeof(float) * ((4 * L + 1) + (4 * L + 9) + 7 * (size_t)cfg->max_days * (size_t)cfg->nslots + (12 + L) + 1) * n +
-         sizeof(float) * (7 * (size_t)cfg->max_days + 12 + L) * ios + sizeof(int) * ios +
+         sizeof(float) * (7 * (size_t)cfg->max_days + 12 + L) * ios + sizeof(int) * 2 * ios +
          sizeof(int) * 6 * n + sizeof(int64_t) * n + sizeof(double) * H9G_NDIAG + sizeof(int) +
          blocks * PairStore<8, H9G_PLANES>::GBLOCK + sizeof(unsigned) * 16 * (size_t)H9G_PACE_ROWS +
          ord_bytes(n, L, 10);
@@ -1360,7 +1363,7 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
   ctx->n = (size_t)cfg->ncell;
   const size_t n = ctx->n;
   const int L = ctx->L;
-  ctx->ios = round_up(n, H9G_PCPW) + H9G_G2_MAX;
+  ctx->ios = 2 * round_up(n, H9G_PCPW) + 64;
   bool ok = hipStreamCreateWithFlags(&ctx->sc, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&ctx->sx, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&ctx->d_par, sizeof(float) * (4 * L + 1) * n) == hipSuccess &&
@@ -1373,6 +1376,7 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
             hipMalloc(&ctx->d_gid, sizeof(int64_t) * n) == hipSuccess &&
             hipMalloc(&ctx->d_lat, sizeof(float) * n) == hipSuccess &&
             hipMalloc(&ctx->d_perm, sizeof(int) * ctx->ios) == hipSuccess &&
+            hipMalloc(&ctx->d_perm2, sizeof(int) * ctx->ios) == hipSuccess &&
             hipMalloc(&ctx->d_hist, sizeof(int) * n) == hipSuccess;
   if (ok) {
     ok = hipMemset(ctx->d_err, 0, sizeof(int) * 4 * n) == hipSuccess &&
@@ -1634,17 +1638,18 @@ static int pace_mode(const h9g_ctx *ctx, int kind, size_t blocks) {
   return blocks <= (size_t)ctx->ncu * pair_kind_resident(kind) ? 2 : 1;
 }
 
-// Whether an every-cell launch can carry k more cells in a second group for
-// free: a pair kernel kind, and the extra waves fit the launch's last round
-// of resident workgroups.
-static bool g2_fits(const h9g_ctx *ctx, size_t k) {
-  if (k == 0 || k > H9G_G2_MAX || !ctx->sort || !(ctx->kind == 1 || ctx->kind == 4 || ctx->kind == 5)) return false;
+// Whether a year launch of `base` cells on the context's kernel can carry k
+// more cells in a second group for free: a pair kernel kind, and the extra
+// waves fit the launch's last round of resident workgroups.
+static bool g2_fits(const h9g_ctx *ctx, size_t base, size_t k) {
+  if (k == 0 || !ctx->sort || !(ctx->kind == 1 || ctx->kind == 4 || ctx->kind == 5)) return false;
 #if defined(H9G_DUMP_AQ)
   return false;
 #endif
   const size_t C = (size_t)pair_wave_cols(ctx->kind), per = pair_block_cells(ctx->kind);
+  if (round_up(base, C) + k > ctx->ios) return false;
   const size_t slots = (size_t)ctx->ncu * pair_kind_resident(ctx->kind);
-  const size_t b1 = (ctx->n + per - 1) / per, b2 = (round_up(ctx->n, C) + k + per - 1) / per;
+  const size_t b1 = (base + per - 1) / per, b2 = (round_up(base, C) + k + per - 1) / per;
   return (b2 + slots - 1) / slots == (b1 + slots - 1) / slots;
 }
 
@@ -1674,24 +1679,46 @@ struct YearSpec {
   float *ann_dst = nullptr;      // list launches: their annual means into these rows (stride n, cell order)
   float *st = nullptr;           // the cells' state and STOP rows (null: the context's own)
   int *err = nullptr;
-  // every-cell launches of a pair kernel (g2_fits): a second group of the k2
-  // cells h2[0..k2) (host) at year jyear2 from slot2, with state st2/err2,
-  // annual means into ann2 (h9g_run_ordered: a decade's re-runs riding in the
-  // next decade's years)
+  bool bulk = false;             // a list launch that is a year of the context's cells (h9g_run_ordered's
+                                 // first pass without the cells still re-running the decade before): the
+                                 // context's kernel, sort history and diagnostics, as an every-cell launch
+  // launches of a pair kernel (g2_fits): a second group of the k2 cells
+  // h2[0..k2) (host) at year jyear2 from slot2, with state st2/err2, annual
+  // means into ann2 (h9g_run_ordered: a decade's re-runs riding in the next
+  // decade's years)
   const int *h2 = nullptr;
   int k2 = 0, slot2 = 0, jyear2 = 0;
   float *st2 = nullptr, *ann2 = nullptr;
   int *err2 = nullptr;
 };
 
+// The kernel of a list launch of m cells (the cell order's re-runs): the
+// one-column kernel up to H9G_PAIR1_MAX cells (lone waves, one per SIMD);
+// at L = 8 the 11-column kernel up to H9G_PAIR11_LIST cells, where its
+// waves still fit about one round; else the context's pair kernel (the
+// pair kernel for the mixed kind), never solo rounds.  Round 6,
+// tools/list_sweep.py (config 2 / config 3, ms per year): 1,000 cells pair
+// 132.7 / 67.7, pair11 119.7 / 61.3, pair1 97.4 / 50.2; 10,000 cells pair
+// 132.5 / 67.9, pair11 120.0 / 62.3; 20,000 cells 133.6 / 68.5 against
+// 136.3 / 70.3.
+#define H9G_PAIR11_LIST 16384
+static int list_kind(const h9g_ctx *ctx, int m) {
+  if (ctx->kind == 2) return 2;
+  if (m <= H9G_PAIR1_MAX && !getenv("H9G_NO_PAIR1")) return 6;
+  if (ctx->L == 8 && ctx->kind == 1 && m <= H9G_PAIR11_LIST && !getenv("H9G_NO_PAIR11")) return 5;
+  return ctx->kind == 3 ? 1 : ctx->kind;
+}
+
 static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
   const int *d_list = ys.d_list;
   const int m = ys.m;
   if (!ctx || ys.slot < 0 || ys.slot >= ctx->cfg.nslots || ys.jyear < 1861 || ys.jyear > 2299) return H9G_EINVAL;
   if (d_list && (m < 1 || (size_t)m > ctx->n || !ys.ann_dst)) return H9G_EINVAL;
+  if (ys.bulk && (!d_list || ys.st || ctx->kind == 2 || ctx->kind == 3)) return H9G_EINVAL;
   const bool two = ys.k2 > 0;
-  if (two && (d_list || !ys.h2 || !ys.st2 || !ys.err2 || !ys.ann2 || ys.slot2 < 0 || ys.slot2 >= ctx->cfg.nslots ||
-              ys.jyear2 < 1861 || ys.jyear2 > 2299 || !g2_fits(ctx, (size_t)ys.k2)))
+  if (two && ((d_list && !ys.bulk) || !ys.h2 || !ys.st2 || !ys.err2 || !ys.ann2 || ys.slot2 < 0 ||
+              ys.slot2 >= ctx->cfg.nslots || ys.jyear2 < 1861 || ys.jyear2 > 2299 ||
+              !g2_fits(ctx, d_list ? (size_t)m : ctx->n, (size_t)ys.k2)))
     return H9G_EINVAL;
   if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
 #if defined(H9G_DUMP_AQ)
@@ -1731,12 +1758,7 @@ static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
   a.st2 = a.st;
   a.err2 = a.err;
   a.iostride = ios;
-  // the launch's kernel: a list runs on the pair kernel (or the one the
-  // context's shard size chose at L = 10), never split into solo rounds;
-  // short lists (the cell-order re-runs' tails) on the one-column kernel
-  const int kind = d_list ? (m <= H9G_PAIR1_MAX && ctx->kind != 2 && !getenv("H9G_NO_PAIR1") ? 6
-                                                                               : (ctx->kind == 3 ? 1 : ctx->kind))
-                          : ctx->kind;
+  const int kind = d_list && !ys.bulk ? list_kind(ctx, m) : ctx->kind;
   const size_t ncells = d_list ? (size_t)m : ctx->n;
   // slot-ordered forcing and annual sums (row stride ios: the cells plus a
   // second group's slack)
@@ -1745,12 +1767,40 @@ static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
     if (!ctx->d_ann_s) HIPCHK(hipMalloc(&ctx->d_ann_s, sizeof(float) * (12 + ctx->L) * ios));
   }
   const size_t dvar = (size_t)ctx->cfg.max_days * ios;
+  // the second group from the first whole wave after the first group's
+  // cells: its slots of d_perm (in h9g_sort_kernel's order over its own
+  // state), then its year's forcing into them
+  auto second_group = [&](int base, int pcpb) -> int {
+    const int split = (int)round_up((size_t)base, (size_t)pair_wave_cols(kind));
+    HIPCHK(hipMemcpyAsync(ctx->d_perm2 + split, ys.h2, sizeof(int) * ys.k2, hipMemcpyHostToDevice, ctx->sc));
+    H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, split, split + ys.k2, pcpb, ys.st2,
+                 ys.err2, ctx->d_hist, ctx->hist_nsub, ctx->d_perm, ctx->d_perm2);
+    h9g_perm_forcing_kernel<<<perm_forcing_blocks(split, split + ys.k2, pcpb, nt2), 256, 0, ctx->sc>>>(
+        split, split + ys.k2, pcpb, nt2, n, a.fvar, ios, dvar, ctx->d_perm, h9g_forcing_slot(ctx, ys.slot2),
+        ctx->d_forc_s);
+    HIPCHK(hipGetLastError());
+    a.split = split;
+    a.cend = split + ys.k2;
+    a.nt2 = nt2;
+    a.st2 = ys.st2;
+    a.err2 = ys.err2;
+    return 0;
+  };
   if (d_list) {
     const int pcpb = kind == 2 ? H9G_YBLOCK : (int)pair_block_cells(kind);
     a.perm = d_list;
+    if (ctx->sort && kind != 6) {
+      // the list in h9g_sort_kernel's order (its waves' columns take the
+      // same branches), into d_perm, free between every-cell launches
+      H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, m, pcpb, a.st, a.err, ctx->d_hist,
+                   ctx->hist_nsub, ctx->d_perm, d_list);
+      a.perm = ctx->d_perm;
+    }
     h9g_perm_forcing_kernel<<<perm_forcing_blocks(0, m, pcpb, nt), 256, 0, ctx->sc>>>(
-        0, m, pcpb, nt, n, a.fvar, ios, dvar, d_list, a.forc, ctx->d_forc_s);
+        0, m, pcpb, nt, n, a.fvar, ios, dvar, a.perm, a.forc, ctx->d_forc_s);
     HIPCHK(hipGetLastError());
+    if (two)
+      if (int r = second_group(m, pcpb)) return r;
     a.forc = ctx->d_forc_s;
     a.annual = ctx->d_ann_s;
     a.sorted_io = 1;
@@ -1758,17 +1808,17 @@ static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
     const int ns = (int)ctx->n_solo, pcpb = (int)pair_block_cells(ctx->kind);
     if (ctx->kind == 2) {
       H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, n, H9G_YBLOCK, ctx->d_st, ctx->d_err,
-                   ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
+                   ctx->d_hist, ctx->hist_nsub, ctx->d_perm, nullptr);
     } else if (ctx->kind == 3) {
       if (ns > 0)
         H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, ns, H9G_YBLOCK, ctx->d_st,
-                     ctx->d_err, ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
+                     ctx->d_err, ctx->d_hist, ctx->hist_nsub, ctx->d_perm, nullptr);
       if (ns < n)
         H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, ns, n, pcpb, ctx->d_st, ctx->d_err,
-                     ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
+                     ctx->d_hist, ctx->hist_nsub, ctx->d_perm, nullptr);
     } else {
       H9G_DISPATCH(ctx, h9g_sort_kernel, H9G_NXCD, H9G_SORT_THREADS, ctx->sc, n, 0, n, pcpb, ctx->d_st, ctx->d_err,
-                   ctx->d_hist, ctx->hist_nsub, ctx->d_perm);
+                   ctx->d_hist, ctx->hist_nsub, ctx->d_perm, nullptr);
     }
     HIPCHK(hipGetLastError());
     a.perm = ctx->d_perm;
@@ -1787,19 +1837,9 @@ static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
     } else {
       perm_range(0, n, pcpb, nt, a.forc);
     }
-    if (two) {
-      // the second group from the first whole wave after the cells: its slots
-      // of d_perm, then its year's forcing into them
-      const int split = (int)round_up(ctx->n, (size_t)pair_wave_cols(kind));
-      HIPCHK(hipMemcpyAsync(ctx->d_perm + split, ys.h2, sizeof(int) * ys.k2, hipMemcpyHostToDevice, ctx->sc));
-      perm_range(split, split + ys.k2, pcpb, nt2, h9g_forcing_slot(ctx, ys.slot2));
-      a.split = split;
-      a.cend = split + ys.k2;
-      a.nt2 = nt2;
-      a.st2 = ys.st2;
-      a.err2 = ys.err2;
-    }
     HIPCHK(hipGetLastError());
+    if (two)
+      if (int r = second_group(n, pcpb)) return r;
     a.forc = ctx->d_forc_s;
     a.annual = ctx->d_ann_s;
     a.sorted_io = 1;
@@ -1911,7 +1951,7 @@ static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
           ys.k2, n, (int)rows, a.split, ios, a.perm, ctx->d_ann_s, ys.ann2);
     HIPCHK(hipGetLastError());
   }
-  if (!d_list) {
+  if (!d_list || ys.bulk) {
     h9g_diag_kernel<<<1, 1024, 0, ctx->sc>>>((int)ctx->n, ctx->L, ctx->d_ann, ctx->d_st, ctx->d_err, ctx->d_diag);
     HIPCHK(hipGetLastError());
   }
@@ -1981,6 +2021,7 @@ struct OrdBufs {
   OrdDec d[2];
   float *st2 = nullptr;                  // the re-running cells' state and STOP rows
   int *err2 = nullptr;
+  int *d_bulk = nullptr;                 // a first pass's cells when some are left out of it
   int ny_cap = 0;
 };
 
@@ -1993,6 +2034,7 @@ static void ord_free(h9g_ctx *ctx) {
   }
   (void)hipFree(o->st2);
   (void)hipFree(o->err2);
+  (void)hipFree(o->d_bulk);
   delete o;
   ctx->ord = nullptr;
 }
@@ -2004,7 +2046,8 @@ static int ord_alloc(h9g_ctx *ctx, int ny) {
   OrdBufs *o = ctx->ord;
   const size_t n = ctx->n, L = (size_t)ctx->L, srows = (size_t)h9g_state_size(ctx->L), rows = 12 + L;
   bool ok = hipMalloc(&o->st2, sizeof(float) * srows * n) == hipSuccess &&
-            hipMalloc(&o->err2, sizeof(int) * 4 * n) == hipSuccess;
+            hipMalloc(&o->err2, sizeof(int) * 4 * n) == hipSuccess &&
+            hipMalloc(&o->d_bulk, sizeof(int) * (n + 1)) == hipSuccess;
   for (OrdDec &D : o->d) {
     ok = ok && hipMalloc(&D.st0, sizeof(float) * srows * n) == hipSuccess &&
          hipMalloc(&D.guess, sizeof(float) * L * n) == hipSuccess &&
@@ -2027,7 +2070,7 @@ static int ord_alloc(h9g_ctx *ctx, int ny) {
 // Work counters of the last ordered call (h9g_decade_stats, h9g_ordered_stats).
 struct OrdStats {
   int64_t passes = 0, rerun_cells = 0, rerun_cell_years = 0, rerun_launches = 0;
-  int64_t ticks = 0, ride_steps = 0, ride_cell_years = 0, alone_steps = 0, alone_cell_years = 0;
+  int64_t ticks = 0, ride_steps = 0, ride_cell_years = 0, alone_steps = 0, alone_cell_years = 0, excluded = 0;
   std::vector<int64_t> launch_cells, dec_passes;
 };
 
@@ -2210,6 +2253,19 @@ static int ord_finish(h9g_ctx *ctx, OrdDec &D, OrdDec *N, float *annual, int &st
   return 0;
 }
 
+// Cells left out of a decade's first pass (still re-running the decade
+// before): re-run in its first check whatever their input (dirty), and never
+// merged back onto a first-pass trajectory they did not run (their
+// checkpoints' STOP code -1, which no run produces).
+__global__ void __launch_bounds__(256) h9g_exclude_kernel(int k, int n, int ny, const int *__restrict__ list,
+                                                          int *__restrict__ dirty, int *__restrict__ eck) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= k) return;
+  const int c = list[j];
+  dirty[c] = 1;
+  for (int y = 0; y < ny; y++) eck[(size_t)y * 4 * n + c] = -1;
+}
+
 // decades: (first year, years) of each decade the call runs, in order;
 // their years' forcing in slots[0 .. sum of years).
 static int run_ordered_impl(h9g_ctx *ctx, const int32_t *slots, int jyear0,
@@ -2262,12 +2318,44 @@ static int run_ordered_impl(h9g_ctx *ctx, const int32_t *slots, int jyear0,
     HIPCHK(hipMemcpyAsync(D.guess, ctx->d_st + (size_t)2 * L * n, sizeof(float) * (size_t)L * n,
                           hipMemcpyDeviceToDevice, ctx->sc));
     HIPCHK(hipMemsetAsync(D.dirty, 0, sizeof(int) * n, ctx->sc));
-    // pass 0: every cell, each year one launch, P's re-runs riding along
+    // the cells P is still re-running stay out of D's first pass: their end
+    // of P, D's start, is not known yet (they re-run D in its first check);
+    // the others form the first pass's list, and P's re-runs ride in its
+    // launches in the slots this leaves
+    std::vector<int> excl;
+    if (P && P->phase == OrdDec::RERUN && !getenv("H9G_NO_EXCLUDE")) {
+      excl = P->list;
+      std::sort(excl.begin(), excl.end());
+    }
+    int nb = (int)n;
+    if (!excl.empty()) {
+      std::vector<int> bulk;
+      bulk.reserve(n - excl.size());
+      size_t e = 0;
+      for (int c = 0; c < (int)n; c++) {
+        if (e < excl.size() && excl[e] == c) {
+          e++;
+          continue;
+        }
+        bulk.push_back(c);
+      }
+      nb = (int)bulk.size();
+      HIPCHK(hipMemcpy(o->d_bulk, bulk.data(), sizeof(int) * nb, hipMemcpyHostToDevice));
+    }
+    S.excluded += (int64_t)excl.size();
+    // pass 0: each year one launch, P's re-runs riding along
     for (int y = 0; y < D.ny; y++) {
       YearSpec ys;
       ys.slot = slots[D.k0 + y];
       ys.jyear = D.y0 + y;
-      const bool ride = P && P->phase == OrdDec::RERUN && g2_fits(ctx, P->list.size()) && !getenv("H9G_NO_RIDE");
+      if (!excl.empty()) {
+        ys.d_list = o->d_bulk;
+        ys.m = nb;
+        ys.bulk = true;
+        ys.ann_dst = ctx->d_ann;
+      }
+      const bool ride = P && P->phase == OrdDec::RERUN && g2_fits(ctx, (size_t)nb, P->list.size()) &&
+                        !getenv("H9G_NO_RIDE");
       if (ride) {
         ys.h2 = P->list.data();
         ys.k2 = (int)P->list.size();
@@ -2291,6 +2379,12 @@ static int run_ordered_impl(h9g_ctx *ctx, const int32_t *slots, int jyear0,
         if (int r = ord_check(ctx, *P, false, S)) return r;
     }
     D.np = 1;
+    if (!excl.empty()) {
+      HIPCHK(hipMemcpy(D.d_list, excl.data(), sizeof(int) * excl.size(), hipMemcpyHostToDevice));
+      h9g_exclude_kernel<<<(unsigned)((excl.size() + 255) / 256), 256, 0, ctx->sc>>>((int)excl.size(), (int)n, D.ny,
+                                                                                    D.d_list, D.dirty, D.eck);
+      HIPCHK(hipGetLastError());
+    }
     if (P) {                                 // P's remaining re-runs, then its end into D's start
       if (int r = ord_settle(ctx, *P, slots, S)) return r;
       if (int r = ord_finish(ctx, *P, &D, annual, stop_seen)) return r;
@@ -2327,9 +2421,9 @@ static int run_ordered_impl(h9g_ctx *ctx, const int32_t *slots, int jyear0,
   ctx->dec_stats[2] = S.rerun_cell_years;
   ctx->dec_stats[3] = S.rerun_launches;
   ctx->dec_launches = S.launch_cells;
-  const int64_t os[6] = {(int64_t)decs.size(), S.ticks, S.ride_steps, S.ride_cell_years, S.alone_steps,
-                         S.alone_cell_years};
-  std::copy(os, os + 6, ctx->ord_stats);
+  const int64_t os[7] = {(int64_t)decs.size(), S.ticks, S.ride_steps, S.ride_cell_years, S.alone_steps,
+                         S.alone_cell_years, S.excluded};
+  std::copy(os, os + 7, ctx->ord_stats);
   ctx->ord_passes = S.dec_passes;
   // the first STOP of the call (h9g_last_error) or one from before it
   return h9g_sync(ctx);
@@ -2386,7 +2480,7 @@ int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n) {
 int h9g_ordered_stats(h9g_ctx *ctx, int64_t *out, int n) {
   if (!ctx || !out || n < 1) return H9G_EINVAL;
   int m = 0;
-  for (; m < n && m < 6; m++) out[m] = ctx->ord_stats[m];
+  for (; m < n && m < 7; m++) out[m] = ctx->ord_stats[m];
   for (size_t i = 0; m < n && i < ctx->ord_passes.size(); i++) out[m++] = ctx->ord_passes[i];
   return m;
 }

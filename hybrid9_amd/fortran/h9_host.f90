@@ -26,8 +26,11 @@ PROGRAM H9_HOST
 ! cell_order = 1 (default) runs the reference's own order: decade by
 ! decade (HYBRID9.f90:93-130), each land cell's first substep of a decade
 ! reading the smp its predecessor in (y, x) order left behind (HYDROLOGY.
-! f90:270-275, SHARED.f90:198), through h9g_run_decade_ordered -- bit for
-! bit the reference on one rank.  cell_order = 0: every cell its own smp
+! f90:270-275, SHARED.f90:198), through h9g_run_ordered -- bit for bit the
+! reference on one rank.  Every year of a call is staged into its own slot
+! and the call overlaps its decades on the device; ordered_decades > 0 cuts
+! the run into calls of that many decades (HBM: 0.69 GB per 0.5 deg year),
+! 0 (default) makes one call.  cell_order = 0: every cell its own smp
 ! (h9g_run_year per year, isolated-cell semantics, DESIGN.md §1).
 !
 ! Usage:  h9_host [driver.txt] [h9gpu.nml]
@@ -50,11 +53,11 @@ REAL(C_FLOAT) :: zi (0:H9G_LMAX+1)
 ! --- extension namelist ----------------------------------------------------
 CHARACTER (LEN = 512) :: input_mode, case_dir, out_dir, pgf_dir
 INTEGER :: nlayers, grow_on, device, grid, year0, nyears, nc_out, gnx, gny, gnland
-INTEGER :: cell_order
+INTEGER :: cell_order, ordered_decades
 INTEGER(C_INT64_T) :: seed
 NAMELIST /h9gpu/ input_mode, case_dir, out_dir, nlayers, grow_on, device, &
                  grid, year0, nyears, seed, pgf_dir, nc_out, gnx, gny, gnland, &
-                 cell_order
+                 cell_order, ordered_decades
 CHARACTER (LEN = 600, KIND = C_CHAR), TARGET :: pgf_file (7)
 TYPE(C_PTR) :: pgf_ptr (7)
 CHARACTER (LEN = *), PARAMETER :: pgf_var (7) = &
@@ -72,7 +75,7 @@ TYPE(C_PTR) :: ctx
 INTEGER(C_INT) :: rc
 INTEGER :: L, ndays, iyr, jyear, nt, d0, u, i, nslot, nland, nx, ny
 INTEGER :: dsyr, deyr, ndec, k
-INTEGER(C_INT32_T) :: slots (10), passes
+INTEGER(C_INT32_T), ALLOCATABLE :: slots (:), passes (:)
 LOGICAL :: have_driver, have_nml
 CHARACTER (LEN = 512) :: arg
 REAL(C_FLOAT), ALLOCATABLE :: theta_s (:,:), hksat (:,:), bsw (:,:), psi_s (:,:)
@@ -80,6 +83,7 @@ REAL(C_FLOAT), ALLOCATABLE :: Fmax (:), forcing (:,:,:), state (:), annual (:,:)
 INTEGER(C_INT64_T), ALLOCATABLE :: gid (:)
 REAL(C_FLOAT), ALLOCATABLE :: lat (:)
 REAL(C_DOUBLE) :: diag (H9G_NDIAG)
+TYPE(h9g_error) :: err
 INTEGER :: time_BOY (2300-1860+1)
 
 !----------------------------------------------------------------------!
@@ -87,7 +91,7 @@ INTEGER :: time_BOY (2300-1860+1)
 !----------------------------------------------------------------------!
 input_mode = 'synth'; case_dir = ''; out_dir = '.'; pgf_dir = '.'
 nlayers = 8; grow_on = 1; device = 0; grid = 1; year0 = 0; nyears = 0
-nc_out = 1; gnx = 0; gny = 0; gnland = 0; cell_order = 1
+nc_out = 1; gnx = 0; gny = 0; gnland = 0; cell_order = 1; ordered_decades = 0
 PATH_output = '.'
 seed = 20161123_C_INT64_T
 NISURF = 48; iDEC_start = 1; iDEC_end = 1
@@ -186,7 +190,11 @@ END DO
 !----------------------------------------------------------------------!
 ! GPU context.
 !----------------------------------------------------------------------!
-nslot = MERGE (10, 2, cell_order /= 0)     ! a decade's years at once in the reference's order
+nslot = 2                                  ! isolated cells: double-buffered years
+IF (cell_order /= 0) THEN                  ! the reference's order: every year of a call resident
+  nslot = nyears
+  IF (ordered_decades > 0) nslot = MIN (nyears, 10 * ordered_decades)
+END IF
 cfg%ncell = ncell
 cfg%nlayers = L
 cfg%nisurf = NISURF
@@ -228,27 +236,37 @@ OPEN (NEWUNIT = u, FILE = TRIM (out_dir)//'/annual.f32', ACCESS = 'STREAM', &
 d0 = 1
 IF (cell_order /= 0) THEN
   ! HYBRID9.f90:93-130: decade by decade (1901-1910, 1911-1920, ...), cut to
-  ! [year0, year0 + nyears); the decade's forcing staged into its slots,
-  ! then the cells run in the reference's order
-  ALLOCATE (annual_dec (ncell, 12 + L, 10))
+  ! [year0, year0 + nyears); a call's years staged into their slots, then
+  ! the cells run in the reference's order, the decades overlapping
+  ALLOCATE (annual_dec (ncell, 12 + L, nslot), slots (nslot), passes (nslot / 10 + 2))
   dsyr = year0
   DO WHILE (dsyr < year0 + nyears)
+    ! the call's last year: ordered_decades whole decades on from dsyr's
     ! (FLOOR, not integer division, which truncates toward zero: before 1901
     ! the decades are 1891-1900, 1881-1890, ...)
-    deyr = MIN (1901 + 10 * FLOOR (REAL (dsyr - 1901) / 10.0) + 9, year0 + nyears - 1)
-    ndec = deyr - dsyr + 1
+    deyr = year0 + nyears - 1
+    IF (ordered_decades > 0) &
+      deyr = MIN (deyr, 1901 + 10 * (FLOOR (REAL (dsyr - 1901) / 10.0) + ordered_decades) - 1)
+    ndec = deyr - dsyr + 1                   ! years of the call
     DO k = 1, ndec
       slots (k) = k - 1
       CALL stage (k - 1, dsyr + k - 1, d0)
       d0 = d0 + time_BOY (dsyr+k-1859) - time_BOY (dsyr+k-1-1859)
     END DO
-    rc = h9g_run_decade_ordered (ctx, slots, dsyr, ndec, annual_dec, passes)
-    CALL h9g_check_stop (ctx, rc)
-    DO k = 1, ndec
+    rc = h9g_run_ordered (ctx, slots, dsyr, ndec, annual_dec, passes)
+    IF (rc < 0) CALL h9g_check_stop (ctx, rc)
+    iyr = ndec
+    IF (rc > 0) THEN                         ! a STOP: the reference ends in its decade,
+      CALL chk (h9g_last_error (ctx, err))   ! after writing the decades before it
+      iyr = 1901 + 10 * FLOOR (REAL (err%year - 1901) / 10.0) - dsyr
+    END IF
+    DO k = 1, iyr
       annual = annual_dec (:, :, k)
       CALL year_out (dsyr + k - 1)
     END DO
-    WRITE (*,'(A,I5,A,I5,A,I3)') ' decade', dsyr, ' -', deyr, ' in cell order: passes', passes
+    CALL h9g_check_stop (ctx, rc)
+    WRITE (*,'(A,I5,A,I5,A,12I3)') ' years', dsyr, ' -', deyr, ' in cell order: passes per decade', &
+          passes (1:FLOOR (REAL (deyr - 1901) / 10.0) - FLOOR (REAL (dsyr - 1901) / 10.0) + 1)
     dsyr = deyr + 1
   END DO
 ELSE

@@ -196,8 +196,9 @@ int h9g_set_chains(h9g_ctx *ctx, const int32_t *chain);
 int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n);
 /* How the last ordered call overlapped its decades: out[0..n) of decades,
  * year launches of the first passes, re-run years that rode in them and
- * their cell-years, re-run years launched alone and their cell-years, then
- * each decade's passes.  Returns the count written. */
+ * their cell-years, re-run years launched alone and their cell-years, cells
+ * left out of a first pass (still re-running the decade before), then each
+ * decade's passes.  Returns the count written. */
 int h9g_ordered_stats(h9g_ctx *ctx, int64_t *out, int n);
 
 /* --- LCLIM single-site path (HYBRID9.f90:339-480) ---------------------- */

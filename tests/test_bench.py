@@ -67,11 +67,12 @@ def test_config_check_reasons():
         h.make_config(0, zi)
     cfg = h.make_config(67420, zi, nslots=25)
     # 25 resident years of forcing dominate: 7 x 366 x 67,420 x 4 B each, plus
-    # the slot-ordered copy of one of them (h9g_perm_forcing_kernel) and the
-    # cell order's buffers for two decades in flight (h9g_run_ordered: start
-    # state, checkpoints and annual means of 10 years each, ~5.9 KB per cell)
-    fixed = 26 * 7 * 366 * 67420 * 4
-    assert fixed + 2 * 10 * (41 + 20) * 4 * 67420 < h.config_bytes(cfg) < 1.01 * fixed + 50e6 + 5.9e3 * 67420
+    # the slot-ordered copy of one year with room for a second group of cells
+    # (h9g_perm_forcing_kernel, twice the cells) and the cell order's buffers
+    # for two decades in flight (h9g_run_ordered: start state, checkpoints and
+    # annual means of 10 years each, ~5.9 KB per cell)
+    fixed = 27 * 7 * 366 * 67420 * 4
+    assert fixed + 2 * 10 * (41 + 20) * 4 * 67420 < h.config_bytes(cfg) < 1.01 * fixed + 60e6 + 5.9e3 * 67420
 
 
 class StubCtx:
