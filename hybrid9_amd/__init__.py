@@ -385,7 +385,8 @@ class Context:
         out = (C.c_int64 * 64)()
         m = _check(self._lib.h9g_ordered_stats(self._h, out, 64), "h9g_ordered_stats")
         keys = ("decades", "first_pass_launches", "rerun_years_riding", "rerun_cell_years_riding",
-                "rerun_years_alone", "rerun_cell_years_alone", "cells_left_out_of_first_pass")
+                "rerun_years_alone", "rerun_cell_years_alone", "cells_left_out_of_first_pass",
+                "probed", "probe_kept")
         d = {k: int(out[i]) for i, k in enumerate(keys)}
         d["passes"] = [int(out[i]) for i in range(len(keys), m)]
         return d
@@ -393,9 +394,9 @@ class Context:
     def launch_stats(self, reset: bool = False) -> dict:
         """Year launches per kernel kind since the last reset
         (h9g_launch_stats): launches, cell-years, device ms."""
-        out = (C.c_double * 18)()
-        m = _check(self._lib.h9g_launch_stats(self._h, out, 18, int(reset)), "h9g_launch_stats")
-        names = ("pair", "solo", "mixed", "pair2", "pair11", "pair1")
+        out = (C.c_double * 21)()
+        m = _check(self._lib.h9g_launch_stats(self._h, out, 21, int(reset)), "h9g_launch_stats")
+        names = ("pair", "solo", "mixed", "pair2", "pair11", "pair1", "probe")
         return {nm: dict(launches=int(out[3 * i]), cell_years=int(out[3 * i + 1]), ms=float(out[3 * i + 2]))
                 for i, nm in enumerate(names) if 3 * i + 2 < m and out[3 * i] > 0}
 

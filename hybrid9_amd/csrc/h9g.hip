@@ -99,6 +99,8 @@ struct KArgs {
   float *__restrict__ st2;
   int *__restrict__ err2;
   size_t iostride;                 // row stride of forc and annual when sorted_io (slots)
+  int raw;                         // 1: the annual rows are the running sums, undivided (the cell
+                                   // order's day-1 probe, h9g_probe_cmp_kernel)
 };
 
 // XCD-aware workgroup order.  MI355X deals the workgroups of a launch
@@ -232,12 +234,12 @@ __device__ __forceinline__ void pair_body(const KArgs &a, const G &g) {
   StampProf pr{stamp_clock(), {0, 0, 0, 0, 0, 0, 0, 0}};
   const int code = cell_year_pair<L, G, Split2, PS, true>(g, cs, sp, s, (const gbl_float *)(a.forc + io), ios, a.fvar, nt,
                                                          a.nisurf, a.grow_on, (gbl_float *)(a.annual + io), ios, eday,
-                                                         estep, errval, T, pr);
+                                                         estep, errval, T, a.raw, pr);
   if (lane == 0 && a.stamps)
     for (int k = 0; k < 8; k++) a.stamps[(blockIdx.x * H9G_PWAVES + wave) * 8 + k] = pr.acc[k];
 #else
   const int code = cell_year_pair<L, G>(g, cs, sp, s, (const gbl_float *)(a.forc + io), ios, a.fvar, nt, a.nisurf,
-                                        a.grow_on, (gbl_float *)(a.annual + io), ios, eday, estep, errval, T);
+                                        a.grow_on, (gbl_float *)(a.annual + io), ios, eday, estep, errval, T, a.raw);
 #endif
   if (spare || h != 0) return;       // the even lane writes the cell back
   int cw = c, iow = io;
@@ -375,7 +377,7 @@ h9g_solo_kernel(const KArgs a, const G g) {
   float errval = 0.0f;
   const int code = cell_year_pair<L, G, SplitAll, SS, false>(g, cs, sp, s, (const gbl_float *)(a.forc + io), ios, a.fvar,
                                                              a.nt, a.nisurf, a.grow_on, (gbl_float *)(a.annual + io),
-                                                             ios, eday, estep, errval, T);
+                                                             ios, eday, estep, errval, T, a.raw);
   int cw = c, iow = io;
   opaque(cw);
   opaque(iow);
@@ -477,13 +479,40 @@ __global__ void __launch_bounds__(256) h9g_chain_kernel(int m, int n, int L, con
   const int k = chain[j];
   const float *src = first[j] ? st0 : st;
   const int p = pred[j];
-  int differ = dirty ? dirty[k] : 0;
+  int differ = 0;
   for (int i = 0; i < L; i++) {
     const float v = src[(size_t)(2 * L + i) * n + p];
     differ |= __float_as_uint(v) != __float_as_uint(guess[(size_t)i * n + k]);
     guess[(size_t)i * n + k] = v;
   }
-  flag[j] = differ;
+  flag[j] = differ | (dirty && dirty[k] ? 2 : 0);   // 1: input changed, 2: start changed
+}
+
+// The cell order's day-1 probe (round 6).  The input smp reaches a cell only
+// through beta of its decade's first substep (HYDROLOGY.f90:270-275).  A
+// cell whose input changed ran the day from its old and from its new input
+// (one-day list launches from the decade's start, running sums undivided,
+// KArgs::raw): if the two agree bit for bit at the day's end -- every state
+// row, the STOP record and every running sum of the year's means -- the
+// days after it and so the whole decade are the same from either input, and
+// the cell needs no re-run (its trajectory is already the one its new input
+// gives).  keep[j] = 1: they differ, the cell re-runs.
+__global__ void __launch_bounds__(256) h9g_probe_cmp_kernel(int m, int n, int srows, int rows,
+                                                            const int *__restrict__ list,
+                                                            const float *__restrict__ stA, const float *__restrict__ stB,
+                                                            const int *__restrict__ errA, const int *__restrict__ errB,
+                                                            const float *__restrict__ annA,
+                                                            const float *__restrict__ annB, int *__restrict__ keep) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const int c = list[j];
+  bool same = true;
+  for (int r = 0; r < srows; r++)
+    same &= __float_as_uint(stA[(size_t)r * n + c]) == __float_as_uint(stB[(size_t)r * n + c]);
+  for (int r = 0; r < 4; r++) same &= errA[(size_t)r * n + c] == errB[(size_t)r * n + c];
+  for (int r = 0; r < rows; r++)
+    same &= __float_as_uint(annA[(size_t)r * n + c]) == __float_as_uint(annB[(size_t)r * n + c]);
+  keep[j] = !same;
 }
 
 // Pipelined decades (h9g_run_ordered): decade D+1's first pass starts from
@@ -1089,7 +1118,8 @@ struct h9g_ctx {
   int64_t ev_cells[NEVT] = {};
   double kstat[8][3] = {};        // per kernel kind: launches, cell-years, ms (h9g_launch_stats)
   struct OrdBufs *ord = nullptr;  // h9g_run_ordered's decade buffers
-  int64_t ord_stats[7] = {};      // last ordered call (h9g_ordered_stats)
+  int64_t ord_stats[9] = {};      // last ordered call (h9g_ordered_stats)
+  int ord_probe = 1;              // the checks' day-1 probe (H9G_NO_PROBE: off)
   std::vector<int64_t> ord_passes;
 };
 
@@ -1427,6 +1457,7 @@ h9g_ctx *h9g_create(const h9g_config *cfg, int device) {
   // time for this many columns (l10_kind)
   if (const char *se = getenv("H9G_SORT")) ctx->sort = atoi(se) != 0;
   if (const char *se = getenv("H9G_PRIO")) ctx->prio_mode = atoi(se);
+  if (getenv("H9G_NO_PROBE")) ctx->ord_probe = 0;
   const char *kenv = getenv("H9G_KERNEL");
   int ncu = 256;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1)
@@ -1623,6 +1654,8 @@ static int join_prefetch(h9g_ctx *ctx, int slot) {
 
 // Columns per wave of a pair-kernel kind: 22, 11 (kind 5, h9g_pair11_kernel)
 // or 1 (kind 6, h9g_pair1_kernel); 4 waves per workgroup.
+// Launch-statistics row of the cell order's day-1 probes (h9g_launch_stats)
+#define H9G_KIND_PROBE 7
 static int pair_wave_cols(int kind) { return kind == 5 ? H9G_PCPW11 : (kind == 6 ? 1 : H9G_PCPW); }
 static size_t pair_block_cells(int kind) { return (size_t)pair_wave_cols(kind) * H9G_PWAVES; }
 // Workgroups of a pair-kernel kind resident per CU (= waves per SIMD).
@@ -1690,6 +1723,10 @@ struct YearSpec {
   int k2 = 0, slot2 = 0, jyear2 = 0;
   float *st2 = nullptr, *ann2 = nullptr;
   int *err2 = nullptr;
+  // list launches: only the year's first `ndays` days (0: all), the annual
+  // rows as undivided running sums (the cell order's day-1 probe)
+  int ndays = 0;
+  bool probe = false;
 };
 
 // The kernel of a list launch of m cells (the cell order's re-runs): the
@@ -1715,6 +1752,7 @@ static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
   if (!ctx || ys.slot < 0 || ys.slot >= ctx->cfg.nslots || ys.jyear < 1861 || ys.jyear > 2299) return H9G_EINVAL;
   if (d_list && (m < 1 || (size_t)m > ctx->n || !ys.ann_dst)) return H9G_EINVAL;
   if (ys.bulk && (!d_list || ys.st || ctx->kind == 2 || ctx->kind == 3)) return H9G_EINVAL;
+  if (ys.probe && (!d_list || ys.bulk || !ys.st || ys.k2 > 0 || ys.ndays < 1)) return H9G_EINVAL;
   const bool two = ys.k2 > 0;
   if (two && ((d_list && !ys.bulk) || !ys.h2 || !ys.st2 || !ys.err2 || !ys.ann2 || ys.slot2 < 0 ||
               ys.slot2 >= ctx->cfg.nslots || ys.jyear2 < 1861 || ys.jyear2 > 2299 ||
@@ -1727,7 +1765,8 @@ static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
   if (const int prc = join_prefetch(ctx, ys.slot)) return prc;
   if (two)
     if (const int prc = join_prefetch(ctx, ys.slot2)) return prc;
-  const int nt = days_in_year(ys.jyear), nt2 = two ? days_in_year(ys.jyear2) : nt;
+  const int nt = ys.probe ? std::min(ys.ndays, days_in_year(ys.jyear)) : days_in_year(ys.jyear);
+  const int nt2 = two ? days_in_year(ys.jyear2) : nt;
   if (ctx->slot_days[ys.slot] < nt || (two && ctx->slot_days[ys.slot2] < nt2)) return H9G_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
   HIPCHK(hipStreamWaitEvent(ctx->sc, ctx->ev_copied[ys.slot], 0));
@@ -1758,6 +1797,7 @@ static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
   a.st2 = a.st;
   a.err2 = a.err;
   a.iostride = ios;
+  a.raw = ys.probe ? 1 : 0;
   const int kind = d_list && !ys.bulk ? list_kind(ctx, m) : ctx->kind;
   const size_t ncells = d_list ? (size_t)m : ctx->n;
   // slot-ordered forcing and annual sums (row stride ios: the cells plus a
@@ -1909,7 +1949,7 @@ static int run_year_impl(h9g_ctx *ctx, const YearSpec &ys) {
   }
 #endif
   const int e = ctx->nev++;
-  ctx->ev_kind[e] = kind;
+  ctx->ev_kind[e] = ys.probe ? H9G_KIND_PROBE : kind;
   ctx->ev_cells[e] = (int64_t)ncells + (two ? ys.k2 : 0);
   HIPCHK(hipEventRecord(ctx->ev0[e], ctx->sc));
   if (kind == 2) {
@@ -2022,6 +2062,10 @@ struct OrdBufs {
   float *st2 = nullptr;                  // the re-running cells' state and STOP rows
   int *err2 = nullptr;
   int *d_bulk = nullptr;                 // a first pass's cells when some are left out of it
+  // the day-1 probe (h9g_probe_cmp_kernel): the inputs the checked cells'
+  // trajectories started from, the probe list and its two runs
+  float *gold = nullptr, *pst = nullptr, *pann = nullptr;
+  int *perr = nullptr, *d_plist = nullptr, *d_pkeep = nullptr;
   int ny_cap = 0;
 };
 
@@ -2035,6 +2079,8 @@ static void ord_free(h9g_ctx *ctx) {
   (void)hipFree(o->st2);
   (void)hipFree(o->err2);
   (void)hipFree(o->d_bulk);
+  for (float *p : {o->gold, o->pst, o->pann}) (void)hipFree(p);
+  for (int *p : {o->perr, o->d_plist, o->d_pkeep}) (void)hipFree(p);
   delete o;
   ctx->ord = nullptr;
 }
@@ -2047,7 +2093,13 @@ static int ord_alloc(h9g_ctx *ctx, int ny) {
   const size_t n = ctx->n, L = (size_t)ctx->L, srows = (size_t)h9g_state_size(ctx->L), rows = 12 + L;
   bool ok = hipMalloc(&o->st2, sizeof(float) * srows * n) == hipSuccess &&
             hipMalloc(&o->err2, sizeof(int) * 4 * n) == hipSuccess &&
-            hipMalloc(&o->d_bulk, sizeof(int) * (n + 1)) == hipSuccess;
+            hipMalloc(&o->d_bulk, sizeof(int) * (n + 1)) == hipSuccess &&
+            hipMalloc(&o->gold, sizeof(float) * L * n) == hipSuccess &&
+            hipMalloc(&o->pst, sizeof(float) * 2 * srows * n) == hipSuccess &&
+            hipMalloc(&o->pann, sizeof(float) * 2 * rows * n) == hipSuccess &&
+            hipMalloc(&o->perr, sizeof(int) * 2 * 4 * n) == hipSuccess &&
+            hipMalloc(&o->d_plist, sizeof(int) * (n + 1)) == hipSuccess &&
+            hipMalloc(&o->d_pkeep, sizeof(int) * (n + 1)) == hipSuccess;
   for (OrdDec &D : o->d) {
     ok = ok && hipMalloc(&D.st0, sizeof(float) * srows * n) == hipSuccess &&
          hipMalloc(&D.guess, sizeof(float) * L * n) == hipSuccess &&
@@ -2071,6 +2123,7 @@ static int ord_alloc(h9g_ctx *ctx, int ny) {
 struct OrdStats {
   int64_t passes = 0, rerun_cells = 0, rerun_cell_years = 0, rerun_launches = 0;
   int64_t ticks = 0, ride_steps = 0, ride_cell_years = 0, alone_steps = 0, alone_cell_years = 0, excluded = 0;
+  int64_t probed = 0, probe_kept = 0;
   std::vector<int64_t> launch_cells, dec_passes;
 };
 
@@ -2125,19 +2178,76 @@ static int ord_chain(h9g_ctx *ctx, OrdDec &D, const std::vector<char> &land) {
 // of the decade as known now (the last year's checkpoint); the flagged cells
 // back to the decade's start on the re-run rows st2 (phase RERUN), or, with
 // none flagged, D has settled.
-static int ord_check(h9g_ctx *ctx, OrdDec &D, bool use_dirty, OrdStats &S) {
+// The day-1 probe of the cells in `cand` (their input changed, their start
+// did not): each runs its decade's first day from the smp its trajectory
+// started from (o->gold) and from its new one (D.guess); the cells whose two
+// days differ are appended to D.list (h9g_probe_cmp_kernel).
+static int ord_probe(h9g_ctx *ctx, OrdDec &D, const int32_t *slots, const std::vector<int> &cand, OrdStats &S) {
+  OrdBufs *o = ctx->ord;
+  const int n = (int)ctx->n, L = ctx->L, k = (int)cand.size();
+  const int rows = 12 + L, srows = h9g_state_size(L);
+  HIPCHK(hipMemcpyAsync(o->d_plist, cand.data(), sizeof(int) * k, hipMemcpyHostToDevice, ctx->sc));
+  for (int v = 0; v < 2; v++) {
+    float *st = o->pst + (size_t)v * srows * n;
+    int *err = o->perr + (size_t)v * 4 * n;
+    h9g_restart_kernel<<<(unsigned)((k + 255) / 256), 256, 0, ctx->sc>>>(k, n, L, o->d_plist, D.st0, D.err0,
+                                                                        v ? D.guess : o->gold, st, err);
+    HIPCHK(hipGetLastError());
+    YearSpec ys;
+    ys.slot = slots[D.k0];
+    ys.jyear = D.y0;
+    ys.d_list = o->d_plist;
+    ys.m = k;
+    ys.ann_dst = o->pann + (size_t)v * rows * n;
+    ys.st = st;
+    ys.err = err;
+    ys.ndays = 1;
+    ys.probe = true;
+    if (int r = run_year_impl(ctx, ys)) return r;
+  }
+  h9g_probe_cmp_kernel<<<(unsigned)((k + 255) / 256), 256, 0, ctx->sc>>>(
+      k, n, srows, rows, o->d_plist, o->pst, o->pst + (size_t)srows * n, o->perr, o->perr + (size_t)4 * n, o->pann,
+      o->pann + (size_t)rows * n, o->d_pkeep);
+  HIPCHK(hipGetLastError());
+  std::vector<int> keep(k);
+  HIPCHK(hipMemcpyAsync(keep.data(), o->d_pkeep, sizeof(int) * k, hipMemcpyDeviceToHost, ctx->sc));
+  HIPCHK(hipStreamSynchronize(ctx->sc));
+  int kept = 0;
+  for (int j = 0; j < k; j++)
+    if (keep[j]) {
+      D.list.push_back(cand[j]);
+      kept++;
+    }
+  S.probed += k;
+  S.probe_kept += kept;
+  return 0;
+}
+
+static int ord_check(h9g_ctx *ctx, OrdDec &D, const int32_t *slots, bool use_dirty, OrdStats &S) {
   OrdBufs *o = ctx->ord;
   const int n = (int)ctx->n, L = ctx->L, m = D.m;
   D.list.clear();
   if (m > 0) {
+    // the inputs the trajectories started from, for the probe
+    HIPCHK(hipMemcpyAsync(o->gold, D.guess, sizeof(float) * L * n, hipMemcpyDeviceToDevice, ctx->sc));
     h9g_chain_kernel<<<(unsigned)((m + 255) / 256), 256, 0, ctx->sc>>>(m, n, L, D.d_chain, D.d_pred, D.d_first,
                                                                       ord_ck(ctx, D, D.ny - 1), D.st0, D.guess,
                                                                       use_dirty ? D.dirty : nullptr, D.d_flag);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(D.flag.data(), D.d_flag, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->sc));
     HIPCHK(hipStreamSynchronize(ctx->sc));
-    for (int j = 0; j < m; j++)
-      if (D.flag[j]) D.list.push_back(D.chain[j]);
+    std::vector<int> cand;
+    const bool probe = ctx->ord_probe;
+    for (int j = 0; j < m; j++) {
+      if (probe && D.flag[j] == 1)
+        cand.push_back(D.chain[j]);
+      else if (D.flag[j])
+        D.list.push_back(D.chain[j]);
+    }
+    if (!cand.empty()) {
+      if (int r = ord_probe(ctx, D, slots, cand, S)) return r;
+      std::sort(D.list.begin(), D.list.end());
+    }
   }
   if (D.list.empty()) {
     D.phase = OrdDec::SETTLED;
@@ -2204,7 +2314,7 @@ static int ord_run_alone(h9g_ctx *ctx, OrdDec &D, const int32_t *slots, OrdStats
 // Runs D's checks and re-runs until it has settled.
 static int ord_settle(h9g_ctx *ctx, OrdDec &D, const int32_t *slots, OrdStats &S) {
   while (D.phase != OrdDec::SETTLED) {
-    const int r = D.phase == OrdDec::CHECK ? ord_check(ctx, D, false, S) : ord_run_alone(ctx, D, slots, S);
+    const int r = D.phase == OrdDec::CHECK ? ord_check(ctx, D, slots, false, S) : ord_run_alone(ctx, D, slots, S);
     if (r) return r;
   }
   return 0;
@@ -2376,7 +2486,7 @@ static int run_ordered_impl(h9g_ctx *ctx, const int32_t *slots, int jyear0,
         if (int r = ord_after_run(ctx, *P, S)) return r;
       }
       if (P && P->phase == OrdDec::CHECK)    // P's next pass starts in time for the next launch
-        if (int r = ord_check(ctx, *P, false, S)) return r;
+        if (int r = ord_check(ctx, *P, slots, false, S)) return r;
     }
     D.np = 1;
     if (!excl.empty()) {
@@ -2394,11 +2504,11 @@ static int run_ordered_impl(h9g_ctx *ctx, const int32_t *slots, int jyear0,
     // D's first check (its cells whose start changed flagged too) and the
     // year-1 re-run of every cell whose input changed
     if (int r = ord_chain(ctx, D, land)) return r;
-    if (int r = ord_check(ctx, D, true, S)) return r;
+    if (int r = ord_check(ctx, D, slots, true, S)) return r;
     if (D.phase == OrdDec::RERUN)
       if (int r = ord_run_alone(ctx, D, slots, S)) return r;
     if (D.phase == OrdDec::CHECK)
-      if (int r = ord_check(ctx, D, false, S)) return r;
+      if (int r = ord_check(ctx, D, slots, false, S)) return r;
     P = &D;
   }
   if (int r = ord_settle(ctx, *P, slots, S)) return r;
@@ -2421,9 +2531,9 @@ static int run_ordered_impl(h9g_ctx *ctx, const int32_t *slots, int jyear0,
   ctx->dec_stats[2] = S.rerun_cell_years;
   ctx->dec_stats[3] = S.rerun_launches;
   ctx->dec_launches = S.launch_cells;
-  const int64_t os[7] = {(int64_t)decs.size(), S.ticks, S.ride_steps, S.ride_cell_years, S.alone_steps,
-                         S.alone_cell_years, S.excluded};
-  std::copy(os, os + 7, ctx->ord_stats);
+  const int64_t os[9] = {(int64_t)decs.size(), S.ticks, S.ride_steps, S.ride_cell_years, S.alone_steps,
+                         S.alone_cell_years, S.excluded, S.probed, S.probe_kept};
+  std::copy(os, os + 9, ctx->ord_stats);
   ctx->ord_passes = S.dec_passes;
   // the first STOP of the call (h9g_last_error) or one from before it
   return h9g_sync(ctx);
@@ -2480,7 +2590,7 @@ int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n) {
 int h9g_ordered_stats(h9g_ctx *ctx, int64_t *out, int n) {
   if (!ctx || !out || n < 1) return H9G_EINVAL;
   int m = 0;
-  for (; m < n && m < 7; m++) out[m] = ctx->ord_stats[m];
+  for (; m < n && m < 9; m++) out[m] = ctx->ord_stats[m];
   for (size_t i = 0; m < n && i < ctx->ord_passes.size(); i++) out[m++] = ctx->ord_passes[i];
   return m;
 }
@@ -2489,7 +2599,7 @@ int h9g_launch_stats(h9g_ctx *ctx, double *out, int n, int reset) {
   if (!ctx || !out || n < 1) return H9G_EINVAL;
   if (int r = fold_events(ctx)) return r;
   int m = 0;
-  for (int k = 1; k <= 6; k++)
+  for (int k = 1; k <= H9G_KIND_PROBE; k++)
     for (int j = 0; j < 3 && m < n; j++) out[m++] = ctx->kstat[k][j];
   if (reset)
     for (auto &row : ctx->kstat) row[0] = row[1] = row[2] = 0.0;

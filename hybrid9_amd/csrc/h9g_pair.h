@@ -2010,7 +2010,8 @@ H9K_HD int substep_pair(const G &g, CS cs, const SP &sp, St<L> &s, float &rnf_su
 template <int L, class G, class SP, class CS, bool Park = true, class PR = NoProf>
 H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_float *forc, size_t fday,
                           size_t fvar, int nt, int nisurf, int grow_on, gbl_float *acc, size_t astride,
-                          int &eday, int &estep, float &errval, const h9m::Tabs &T, PR &&pr = PR()) {
+                          int &eday, int &estep, float &errval, const h9m::Tabs &T, int raw = 0,
+                          PR &&pr = PR()) {
   enum { A_NPP = 0, A_PM, A_RNF, A_EVAP, A_TAS, A_RLDS, A_RSDS, A_HUSS, A_PS, A_PR, A_RHS,
          A_THETA, A_H2O = 11 + L };
   gbl_float *A = acc;
@@ -2131,6 +2132,10 @@ H9K_HD int cell_year_pair(const G &g, CS cs, const SP &sp, St<L> &s, const gbl_f
   // :263-290
   if (!act) return 0;
   opaque(A);
+  if (raw) {                   // the cell order's day-1 probe: the running sums themselves
+    A[A_RNF * as] = rnf_sum;
+    return 0;
+  }
   A[A_PM * as] = A[A_PM * as] / (float)nt;
   A[A_RNF * as] = rnf_sum / (float)(nt * nisurf);
   A[A_EVAP * as] = zero / (float)(nt * nisurf);

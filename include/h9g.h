@@ -197,7 +197,8 @@ int h9g_decade_stats(h9g_ctx *ctx, int64_t *out, int n);
 /* How the last ordered call overlapped its decades: out[0..n) of decades,
  * year launches of the first passes, re-run years that rode in them and
  * their cell-years, re-run years launched alone and their cell-years, cells
- * left out of a first pass (still re-running the decade before), then each
+ * left out of a first pass (still re-running the decade before), cells the
+ * checks' day-1 probe ran and those of them it kept for a re-run, then each
  * decade's passes.  Returns the count written. */
 int h9g_ordered_stats(h9g_ctx *ctx, int64_t *out, int n);
 
@@ -308,8 +309,9 @@ double h9g_total_kernel_ms(h9g_ctx *ctx, int reset);
 const char *h9g_kernel_name(h9g_ctx *ctx);
 /* Per kernel kind 1..6 (pair, solo, solo+pair, pair2, pair11, pair1 -- the
  * one-column kernel of short re-run lists), 3 doubles each: year launches,
- * cell-years and device ms since the last reset (synchronises).  Returns the
- * count written (<= 18). */
+ * cell-years and device ms since the last reset (synchronises); then row 7,
+ * the cell order's one-day probe launches (launches, cells, ms).  Returns
+ * the count written (<= 21). */
 int h9g_launch_stats(h9g_ctx *ctx, double *out, int n, int reset);
 /* Digest of the sources and compile flags of this library (16 hex digits;
  * hybrid9_amd/build.py build_id).  Profiles record it, and the bench

@@ -157,6 +157,30 @@ def test_gpu_cell_order_matches_reference(name, pipelined):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["co_band", "co_c2_band"])
+def test_gpu_cell_order_probe_keeps_results(name, monkeypatch):
+    """The checks' day-1 probe (h9g_probe_cmp_kernel, round 6) drops from a
+    re-run every cell whose first day from its new input equals the day
+    from its old one; the results stay the reference's bit for bit, with
+    and without it (H9G_NO_PROBE), and the probe re-runs fewer cell-years."""
+    import hybrid9_amd as h
+    meta, inp, exp = load_golden(name)
+    out = h.run_cell_order(**inp)
+    monkeypatch.setenv("H9G_NO_PROBE", "1")
+    ref = h.run_cell_order(**inp)
+    for o in (out, ref):
+        assert o["rc"] == 0, o["err"]
+        assert same_bits(o["annual"], exp["annual"])
+        assert same_bits(o["state"], exp["state"])
+    ov, ov0 = out["overlap"], ref["overlap"]
+    yrs, yrs0 = out["work"][0]["rerun_cell_years"], ref["work"][0]["rerun_cell_years"]
+    print(f"{name}: probe ran {ov['probed']} cells, kept {ov['probe_kept']} for a re-run; cell-years re-run "
+          f"{yrs} (without the probe {yrs0}); passes {out['passes']} / {ref['passes']}")
+    assert ov0["probed"] == 0 and 0 < ov["probe_kept"] < ov["probed"]
+    assert yrs < yrs0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("pipelined", [True, False], ids=["run_ordered", "per_decade"])
 def test_gpu_cell_order_blocks_match_reference(pipelined):
     """One context holding the 4 reference ranks' blocks as 4 chains
