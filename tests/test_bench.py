@@ -115,6 +115,67 @@ def _worker(rank, world, port_no, q):
     dist.destroy_process_group()
 
 
+class StubOrderedCtx(StubCtx):
+    """The cell order's calls (bench.ordered_years): run_ordered records the
+    years of each call; the stats are those of an empty call."""
+
+    def run_ordered(self, slots, year0, raise_on_stop=True, annual=True):
+        for k, s in enumerate(slots):
+            self.years.append((s, year0 + k))
+        self.ms += len(slots)
+        return None, [1] * len(h.decades(year0, len(slots)))
+
+    def decade_stats(self):
+        return dict(passes=1, rerun_cells=0, rerun_cell_years=0, rerun_launches=0, launch_cells=[])
+
+    def ordered_stats(self):
+        return dict(decades=1, passes=[1])
+
+    def launch_stats(self, reset=False):
+        return {}
+
+
+def _worker_cell(rank, world, port_no, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port_no)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    W, K = bench.decade_aligned(5, 20)
+    pl = bench.plan("config2", W, K, world=world, rank=rank)
+    ctx = StubOrderedCtx(rank)
+    exchange, buf = bench.make_exchange(ctx, torch, dist, world, "cpu")
+    work = []
+    elapsed = bench.timed_steps(ctx, pl, exchange, lambda: dist.barrier(), "cell", work)
+    q.put((rank, ctx.years, buf.numpy().copy(), elapsed, len(work), W, K))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_world2_gloo_bench_cell_order():
+    """The driver's command at world size 2 in the default (cell) order:
+    the warm-up rounded to whole decades (1901-1910 untimed), then 1911-1930
+    as one h9g_run_ordered call per rank between two barriers, and the
+    diagnostics all-reduced after each call."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port_no = _free_port()
+    procs = [ctx.Process(target=_worker_cell, args=(r, 2, port_no, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    want = sum(np.arange(h.NDIAG, dtype=np.float64) * (r + 1) + 1930 for r in range(2))
+    for rank, years, buf, elapsed, ncalls, W, K in res:
+        assert (W, K) == (10, 20)
+        assert [y for _, y in years] == list(range(1901, 1931))
+        assert ncalls == 1                               # the timed call's stats only
+        np.testing.assert_array_equal(buf, want)
+        assert elapsed >= 0
+    with pytest.raises(SystemExit):
+        bench.decade_aligned(5, 15)                      # a cut decade is refused
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
