@@ -1314,7 +1314,9 @@ static size_t ord_bytes(size_t n, size_t L, size_t ny) {
   const size_t srows = 4 * L + 9, rows = 12 + L;
   return 2 * (sizeof(float) * (srows + L + ny * (rows + srows)) * n + sizeof(int) * (4 + 4 * ny + 1) * n +
               sizeof(int) * 5 * (n + 1)) +
-         sizeof(float) * srows * n + sizeof(int) * (4 * n + n + 1);
+         sizeof(float) * srows * n + sizeof(int) * (4 * n + n + 1) +
+         // the day-1 probe (OrdBufs): old inputs, two runs' state, sums and STOP rows, list, flags
+         sizeof(float) * (L + 2 * srows + 2 * rows) * n + sizeof(int) * (8 * n + 2 * (n + 1));
 }
 
 size_t h9g_config_bytes(const h9g_config *cfg) {

@@ -70,9 +70,9 @@ def test_config_check_reasons():
     # the slot-ordered copy of one year with room for a second group of cells
     # (h9g_perm_forcing_kernel, twice the cells) and the cell order's buffers
     # for two decades in flight (h9g_run_ordered: start state, checkpoints and
-    # annual means of 10 years each, ~5.9 KB per cell)
+    # annual means of 10 years each, and the day-1 probe's rows: ~6.4 KB per cell)
     fixed = 27 * 7 * 366 * 67420 * 4
-    assert fixed + 2 * 10 * (41 + 20) * 4 * 67420 < h.config_bytes(cfg) < 1.01 * fixed + 60e6 + 5.9e3 * 67420
+    assert fixed + 2 * 10 * (41 + 20) * 4 * 67420 < h.config_bytes(cfg) < 1.01 * fixed + 60e6 + 6.5e3 * 67420
 
 
 class StubCtx:

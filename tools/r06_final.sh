@@ -8,6 +8,8 @@
 #           first passes run), summarised into profiles/pmc_<tag>.json, which
 #           bench.py attaches to runs of the same build
 #   PART=3  config 5: the L = 10 shard table, isolated and in cell order
+#   PART=4  the forced-re-run build (H9G_FORCE_RERUN) on the parity and cell-order tests,
+#           config 3 read from netCDF-4 files
 # Usage: PART=n bash tools/r06_final.sh <tag>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -58,5 +60,16 @@ case "${PART:-1}" in
   echo "== l10 shards (cell order)" && timeout -k 10 700 python3 -u tools/l10_shards.py --ordered \
     > gpurun_out/${TAG}_l10_shards_ordered.txt 2>&1
   rc=$?; cat gpurun_out/${TAG}_l10_shards_ordered.txt; exit $rc
+  ;;
+4)
+  if [ -f hybrid9_amd/lib/libh9g_frr.so ]; then
+    echo "== forced re-run build" && H9G_LIB=hybrid9_amd/lib/libh9g_frr.so timeout -k 10 700 python -u -m pytest \
+      tests/test_gpu_parity.py tests/test_cell_order.py -x -v -m gpu -p no:cacheprovider --timeout 300 \
+      --timeout-method thread -k "golden or stop or nan or config5 or cell_order" > gpurun_out/pytest_frr_$TAG.txt 2>&1
+    rc=$?; tail -2 gpurun_out/pytest_frr_$TAG.txt; [ $rc -eq 0 ] || exit $rc
+  fi
+  echo "== config3 nc4" && timeout -k 10 400 python3 -u bench.py --workload config3 --forcing nc4 --steps 3 --warmup 1 \
+    > gpurun_out/bench_${TAG}_config3_nc4.json 2> gpurun_out/bench_${TAG}_config3_nc4.err
+  rc=$?; tail -c 600 gpurun_out/bench_${TAG}_config3_nc4.json; echo; exit $rc
   ;;
 esac
