@@ -2391,6 +2391,13 @@ static int run_ordered_impl(h9g_ctx *ctx, const int32_t *slots, int jyear0,
   if (nyears < 1 || nymax > ctx->cfg.nslots) return H9G_EINVAL;
   for (int y = 0; y < nyears; y++)
     if (slots[y] < 0 || slots[y] >= ctx->cfg.nslots || jyear0 + y < 1861 || jyear0 + y > 2299) return H9G_EINVAL;
+  {
+    // every year its own slot: a decade's re-runs read their years' forcing
+    // while the next decade's first pass reads its own
+    std::vector<char> used((size_t)ctx->cfg.nslots, 0);
+    for (int y = 0; y < nyears; y++)
+      if (used[(size_t)slots[y]]++) return H9G_EINVAL;
+  }
   if (!ctx->params_set || !ctx->state_set) return H9G_ESTATE;
   const size_t n = ctx->n;
   const int L = ctx->L, rows = 12 + L, srows = h9g_state_size(L);

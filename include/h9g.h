@@ -170,7 +170,8 @@ int h9g_run_decade_ordered(h9g_ctx *ctx, const int32_t *slots, int jyear0,
  * jyear0+nyears-1 (the forcing of year jyear0+k in slots[k], every year's
  * slot resident for the whole call) cut into the reference's decades
  * (1901-1910, 1911-1920, ...), each run as h9g_run_decade_ordered runs
- * one, with the same results bit for bit.  The decades overlap on the
+ * one, with the same results bit for bit.  The years' slots must be
+ * distinct (H9G_EINVAL otherwise).  The decades overlap on the
  * device: a decade's first pass starts as soon as the previous decade's
  * first pass and year-1 re-run are done, and that decade's remaining
  * re-runs ride in its year launches.  annual: (nyears,

@@ -157,6 +157,28 @@ def test_gpu_cell_order_matches_reference(name, pipelined):
 
 
 @pytest.mark.gpu
+def test_gpu_ordered_call_refuses_shared_slots():
+    """Every year of an ordered call keeps its own forcing slot: a decade's
+    re-runs read their years while the next decade's first pass reads its
+    own, so a slot named twice is refused before anything runs."""
+    import hybrid9_amd as h
+    meta, inp, _ = load_golden("co_c1_30yr")
+    L, n = meta["L"], meta["ncell"]
+    with h.Context(n, inp["zi"], nlayers=L, nisurf=inp["nisurf"], grow_on=inp["grow_on"], nslots=3) as ctx:
+        ctx.set_params(inp["params"])
+        ctx.init_state()
+        d0 = 0
+        for k in range(3):
+            nt = h.days_in_year(1901 + k)
+            ctx.push_forcing(k, inp["forcing"][:, d0:d0 + nt, :])
+            d0 += nt
+        with pytest.raises(h.H9GError):
+            ctx.run_ordered([0, 1, 0], 1901)
+        _, passes = ctx.run_ordered([0, 1, 2], 1901)      # distinct slots run
+        assert len(passes) == 1
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["co_band", "co_c2_band"])
 def test_gpu_cell_order_probe_keeps_results(name, monkeypatch):
     """The checks' day-1 probe (h9g_probe_cmp_kernel, round 6) drops from a
