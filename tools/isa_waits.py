@@ -66,7 +66,8 @@ def kind(ins: str) -> str:
 
 def main() -> None:
     stem = Path(sys.argv[1])
-    func = "_Z15h9g_pair_kernelILi8EN3h9k4GeoCILi8ELi48EEEEv5KArgsT0_"
+    pos = [a for a in sys.argv[2:] if not a.startswith("--")]
+    func = pos[0] if pos else "_Z15h9g_pair_kernelILi8EN3h9k4GeoCILi8ELi48EEEEv5KArgsT0_"
     top = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--top=")), 12))
     w, inloop, _, h, _ = weights(stem, func, [])
     blocks, order = blocks_asm(stem, func)
